@@ -1,0 +1,156 @@
+"""ctypes binding of libdprf.so (include/dprf.h) -- the only way Python reaches the verification kernels.
+
+There is no CPU fallback: if the library is missing, ``lib()`` raises; if no gfx950 device is visible,
+context creation raises :class:`DprfError` (DPRF_E_NODEVICE).
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdprf.so")
+
+ABI_VERSION = 1
+FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
+E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
+FLAG_NEVER_MATCHES, FLAG_REF_NONDETERMINISTIC = 1, 2
+MAX_PW, MAX_PW_RANGE = 64, 32
+
+EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_ctx_create", "dprf_ctx_destroy",
+           "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel", "dprf_search_range", "dprf_verify_list"]
+
+
+class DprfError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("dprf error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
+                ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libdprf.so (in-tree).  Raises if it has not been built: never falls back to a CPU path."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError("libdprf.so not found at %s: build it with `python -c 'import __graft_entry__ as g; "
+                                  "g.build()'` (make -C dprf_amd/csrc)" % LIB_PATH)
+            L = ctypes.CDLL(LIB_PATH)
+            L.dprf_abi_version.restype = ctypes.c_int
+            L.dprf_last_error.restype = ctypes.c_char_p
+            L.dprf_device_count.restype = ctypes.c_int
+            L.dprf_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p)]
+            L.dprf_ctx_create.restype = ctypes.c_int
+            L.dprf_ctx_destroy.argtypes = [ctypes.c_void_p]
+            L.dprf_ctx_format.argtypes = [ctypes.c_void_p]
+            L.dprf_ctx_flags.argtypes = [ctypes.c_void_p]
+            L.dprf_ctx_kernel.argtypes = [ctypes.c_void_p]
+            L.dprf_ctx_kernel.restype = ctypes.c_char_p
+            L.dprf_search_range.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
+            L.dprf_search_range.restype = ctypes.c_int
+            L.dprf_verify_list.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
+            L.dprf_verify_list.restype = ctypes.c_int
+            if L.dprf_abi_version() != ABI_VERSION:
+                raise ImportError("libdprf.so ABI %d != %d" % (L.dprf_abi_version(), ABI_VERSION))
+            _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise DprfError(rc, lib().dprf_last_error().decode(errors="replace"))
+
+
+def device_count():
+    return lib().dprf_device_count()
+
+
+def _to_bytes(p):
+    return p.encode("utf-8") if isinstance(p, str) else bytes(p)
+
+
+class Context:
+    """One document on one GPU: the compiled form of the verifier argv brute_force.py builds per
+    candidate (brute_force.py:163-197)."""
+
+    def __init__(self, fields, device=0):
+        fields = list(fields)
+        arr = (ctypes.c_char_p * len(fields))(*[_to_bytes(f) for f in fields])
+        h = ctypes.c_void_p()
+        _check(lib().dprf_ctx_create(arr, len(fields), int(device), ctypes.byref(h)))
+        self._h = h
+        self.fields = fields
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dprf_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def format(self):
+        return lib().dprf_ctx_format(self._h)
+
+    @property
+    def flags(self):
+        return lib().dprf_ctx_flags(self._h)
+
+    @property
+    def kernel(self):
+        return lib().dprf_ctx_kernel(self._h).decode()
+
+    def search_range(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
+        """Verify keyspace indices [start, start+count) of charset^pwlen (itertools.product order).
+        Returns (sorted hit indices (at most cap), total hits, stats dict)."""
+        cs = _to_bytes(charset)
+        hits = (ctypes.c_uint64 * max(1, cap))()
+        nh = ctypes.c_int64()
+        st = Stats()
+        _check(lib().dprf_search_range(self._h, cs, len(cs), int(pwlen), int(start), int(count),
+                                       1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
+        return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()
+
+    def verify_list(self, passwords, stop_on_first=False, cap=1 << 16):
+        """Verify an explicit candidate list (a client payload).  Returns (sorted hit list indices,
+        total hits, stats dict)."""
+        bs = [_to_bytes(p) for p in passwords]
+        offs = [0]
+        for b in bs:
+            offs.append(offs[-1] + len(b))
+        blob = b"".join(bs)
+        o = (ctypes.c_uint64 * len(offs))(*offs)
+        hits = (ctypes.c_uint64 * max(1, cap))()
+        nh = ctypes.c_int64()
+        st = Stats()
+        _check(lib().dprf_verify_list(self._h, blob, o, len(bs), 1 if stop_on_first else 0, hits, cap,
+                                      ctypes.byref(nh), ctypes.byref(st)))
+        return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()

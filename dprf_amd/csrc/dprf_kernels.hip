@@ -1,0 +1,538 @@
+/* dprf_kernels.hip -- gfx950 verification kernels, one candidate per lane.
+ *
+ * Each kernel restates one reference verify() for a batch of candidates:
+ *   k_office   msoffcrypto_password_verifier.c:56-191  (SHA-1 x50,002 + AES-128-ECB check)
+ *   k_odt      odt_password_verifier.c:51-126          (SHA-256, PBKDF2-HMAC-SHA1 x1024, AES-256-CBC)
+ *   k_pdf_r24  pdf_password_verifier.c:134-191         (MD5 [x50] + RC4 [x20], S-box in LDS)
+ *   k_pdf_r5   pdf_password_verifier.c:194-221         (one SHA-256)
+ *   k_pdf_r6   pdf_password_verifier.c:226-291         (dprf_kernels_r6.hip)
+ * Candidates come either from on-device enumeration of a keyspace index (range mode, the
+ * brute_force.py -pr path) or from a packed slot buffer (list mode, the client payload path).
+ * A hit appends its index to a device buffer (atomic), lowers `first` (atomicMin) and, when asked,
+ * raises a stop flag that later launches of the same call observe and skip.
+ */
+#include "dev_crypto.h"
+#include "dprf_params.h"
+#include "dprf_launch.h"
+
+/* ------------------------------------------------------------------ candidate source */
+struct cand {
+    uint32_t w[DPRF_SLOT_WORDS];   /* LE-packed bytes (UTF-16LE code units for Office) */
+    uint32_t len;                  /* bytes */
+};
+
+DEVI uint32_t fastdiv(uint32_t n, uint32_t m, uint32_t s) {
+    uint32_t t = __umulhi(n, m);
+    return (t + ((n - t) >> 1)) >> s;
+}
+
+/* Keyspace index start+g -> candidate, itertools.product order (brute_force.py:205): the digit at
+ * position pwlen-1 varies fastest.  UTF16: emit UTF-16LE code units (Office; ASCII charset only). */
+template <bool UTF16>
+DEVI void range_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand &c) {
+#pragma unroll
+    for (int j = 0; j < DPRF_SLOT_WORDS; j++) c.w[j] = 0;
+    uint32_t rem = g, carry = 0;
+#pragma unroll
+    for (int p = DPRF_MAX_RANGE_LEN - 1; p >= 0; --p) {
+        if ((uint32_t)p < e.pwlen) {
+            uint32_t q = e.cslen == 1 ? rem : fastdiv(rem, e.div_m, e.div_s);
+            uint32_t r = rem - q * e.cslen;
+            uint32_t d = (uint32_t)e.sdig[p] + r + carry;
+            carry = d >= e.cslen ? 1u : 0u;
+            d -= carry ? e.cslen : 0u;
+            rem = q;
+            uint32_t ch = cs[d];
+            if (UTF16) c.w[p >> 1] |= ch << (16 * (p & 1));
+            else c.w[p >> 2] |= ch << (8 * (p & 3));
+        }
+    }
+    c.len = UTF16 ? 2 * e.pwlen : e.pwlen;
+}
+
+DEVI void list_candidate(const dprf_enum &e, uint32_t g, cand &c) {
+    const uint64_t slot = e.start + g;
+    const uint4 *s = (const uint4 *)(e.slots + slot * DPRF_SLOT_WORDS);
+#pragma unroll
+    for (int q = 0; q < DPRF_SLOT_WORDS / 4; q++) {
+        uint4 v = s[q];
+        c.w[4 * q + 0] = v.x; c.w[4 * q + 1] = v.y; c.w[4 * q + 2] = v.z; c.w[4 * q + 3] = v.w;
+    }
+    c.len = e.lens[slot];
+}
+
+template <int MODE, bool UTF16>
+DEVI void get_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand &c) {
+    if (MODE == 0) range_candidate<UTF16>(e, cs, g, c);
+    else list_candidate(e, g, c);
+}
+
+/* ------------------------------------------------------------------ block prologue / epilogue */
+/* Stage the charset (and optionally the AES tables) into LDS, read the stop flag once per block. */
+template <bool AES>
+DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_results *R, uint32_t stop_on_first,
+                         uint8_t *cs, aes_lds *L, uint32_t *flag) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < 64; k += blockDim.x) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
+    if (AES) {
+        for (uint32_t k = tid; k < 256; k += blockDim.x) { L->te[k] = T->te0[k]; L->td[k] = T->td0[k]; }
+        for (uint32_t k = tid; k < 64; k += blockDim.x) {
+            L->sb[k] = ((const uint32_t *)T->sbox)[k];
+            L->isb[k] = ((const uint32_t *)T->inv_sbox)[k];
+        }
+    }
+    if (tid == 0) *flag = stop_on_first ? __hip_atomic_load(&R->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    __syncthreads();
+    return *flag == 0;
+}
+
+DEVI void report_hit(dprf_results *R, unsigned long long idx, uint32_t cap, uint32_t stop_on_first) {
+    uint32_t slot = atomicAdd(&R->nhits, 1u);
+    if (slot < cap) R->hits[slot] = idx;
+    atomicMin(&R->first, idx);
+    if (stop_on_first) atomicExch(&R->stop, 1u);
+}
+
+DEVI void count_block(const dprf_enum &e, dprf_results *R) {
+    if (threadIdx.x == 0) {
+        uint32_t base = blockIdx.x * blockDim.x;
+        uint32_t n = e.count - base < blockDim.x ? e.count - base : blockDim.x;
+        atomicAdd(&R->evaluated, (unsigned long long)n);
+    }
+}
+
+/* BE message words of `len` candidate bytes (LE-packed) placed after `pre` bytes already in m[],
+ * pre a multiple of 4 and <= 16, with the 0x80 terminator.  Static indices only. */
+template <int PREW>
+DEVI void be_append(uint32_t m[32], const cand &c) {
+#pragma unroll
+    for (int j = 0; j < DPRF_SLOT_WORDS; j++)
+        m[PREW + j] = bswap32((c.w[j] & le_keep_mask(j, c.len)) | le_pad80(j, c.len));
+#pragma unroll
+    for (int j = PREW + DPRF_SLOT_WORDS; j < 32; j++) m[j] = 0;
+}
+
+/* SHA-1 / SHA-256 of a <= 119-byte message held in m[32] (BE, already terminated with 0x80):
+ * one or two blocks, chosen per lane. */
+DEVI void sha1_msg2(uint32_t m[32], uint32_t total, uint32_t out[5]) {
+    const uint32_t bits = total * 8u;
+    const bool two = total > 55u;
+    uint32_t b0[16], b1[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) { b0[j] = m[j]; b1[j] = m[16 + j]; }
+    if (!two) b0[15] = bits;
+    b1[15] = bits;
+    sha1_iv(out);
+    sha1_compress(out, b0);
+    if (two) sha1_compress(out, b1);
+}
+DEVI void sha256_msg2(uint32_t m[32], uint32_t total, uint32_t out[8]) {
+    const uint32_t bits = total * 8u;
+    const bool two = total > 55u;
+    uint32_t b0[16], b1[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) { b0[j] = m[j]; b1[j] = m[16 + j]; }
+    if (!two) b0[15] = bits;
+    b1[15] = bits;
+    sha256_iv(out);
+    sha256_compress(out, b0);
+    if (two) sha256_compress(out, b1);
+}
+
+/* ================================================================== Office (ECMA-376 Standard) */
+template <int MODE>
+__global__ void __launch_bounds__(256, 8)
+k_office(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
+         uint32_t stop_on_first) {
+    __shared__ uint8_t cs[256];
+    __shared__ aes_lds L;
+    __shared__ uint32_t flag;
+    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g0 < e.count;
+    const uint32_t g = valid ? g0 : e.count - 1;
+    cand c;
+    get_candidate<MODE, true>(e, cs, g, c);
+
+    /* H0 = SHA1(salt[0:16] || UTF16LE(pw)) (msoffcrypto...c:94-101) */
+    uint32_t m[32];
+    m[0] = p.salt[0]; m[1] = p.salt[1]; m[2] = p.salt[2]; m[3] = p.salt[3];
+    be_append<4>(m, c);
+    uint32_t h[5];
+    sha1_msg2(m, 16u + c.len, h);
+
+    /* 50,000 x H = SHA1(LE32(i) || H) (:105-113): W0 = bswap(i) is wave-uniform */
+    for (uint32_t i = 0; i < 50000u; i++) {
+        uint32_t w[16] = {bswap32(i), h[0], h[1], h[2], h[3], h[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 192u};
+        uint32_t s[5];
+        sha1_iv(s);
+        sha1_compress(s, w);
+        h[0] = s[0]; h[1] = s[1]; h[2] = s[2]; h[3] = s[3]; h[4] = s[4];
+    }
+    /* H = SHA1(H || 00000000) (:115-118) */
+    {
+        uint32_t w[16] = {h[0], h[1], h[2], h[3], h[4], 0u, 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 192u};
+        sha1_iv(h);
+        sha1_compress(h, w);
+    }
+    /* X1 = SHA1((0x36 x 64) ^ H), key = X1[0:16] (:128-153) */
+    uint32_t x1[5];
+    {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = 0x36363636u ^ (j < 5 ? h[j] : 0u);
+        sha1_iv(x1);
+        sha1_compress(x1, w);
+        uint32_t w2[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512u};
+        sha1_compress(x1, w2);
+    }
+    /* AES-128-ECB decrypt of verifier and verifier hash, always AES-128 (:159-172, :207) */
+    uint32_t rk[44], dk[44];
+    aes128_expand(L, x1, rk);
+    aes_dec_schedule<10>(L, rk, dk);
+    uint32_t dv[4], dh0[4], dh1[4];
+    aes_decrypt<10>(L, dk, p.ev, dv);
+    aes_decrypt<10>(L, dk, p.evh, dh0);
+    aes_decrypt<10>(L, dk, p.evh + 4, dh1);
+    /* decryptedVerifierHash[hash_size] == 0 (:168), hash_size uniform in [0,32) */
+    const uint32_t hs = p.hash_size;
+    const uint32_t wi = (hs & 15u) >> 2, sh = 24u - 8u * (hs & 3u);
+    const uint32_t *blk = hs < 16u ? dh0 : dh1;
+    uint32_t word = wi == 0 ? blk[0] : wi == 1 ? blk[1] : wi == 2 ? blk[2] : blk[3];
+    bool ok = ((word >> sh) & 0xffu) == 0u;
+    /* SHA1(verifier) == dec_evh[0:20] (:175-188) */
+    uint32_t vh[5];
+    {
+        uint32_t w[16] = {dv[0], dv[1], dv[2], dv[3], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 128u};
+        sha1_iv(vh);
+        sha1_compress(vh, w);
+    }
+    ok = ok && vh[0] == dh0[0] && vh[1] == dh0[1] && vh[2] == dh0[2] && vh[3] == dh0[3] && vh[4] == dh1[0];
+    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+    count_block(e, R);
+}
+
+/* ================================================================== ODF 1.2 (AES-256-CBC, PBKDF2-HMAC-SHA1) */
+template <int MODE>
+__global__ void __launch_bounds__(256, 8)
+k_odt(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
+      uint32_t stop_on_first) {
+    __shared__ uint8_t cs[256];
+    __shared__ aes_lds L;
+    __shared__ uint32_t flag;
+    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g0 < e.count;
+    const uint32_t g = valid ? g0 : e.count - 1;
+    cand c;
+    get_candidate<MODE, false>(e, cs, g, c);
+
+    /* start key = SHA256(password) (odt...c:78-79) */
+    uint32_t sk[8];
+    {
+        uint32_t m[32];
+        be_append<0>(m, c);
+        sha256_msg2(m, c.len, sk);
+    }
+    /* PBKDF2-HMAC-SHA1(sk, salt, 1024, 32) (:85): ipad/opad midstates once per candidate */
+    uint32_t ist[5], ost[5];
+    {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = 0x36363636u ^ (j < 8 ? sk[j] : 0u);
+        sha1_iv(ist); sha1_compress(ist, w);
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = 0x5c5c5c5cu ^ (j < 8 ? sk[j] : 0u);
+        sha1_iv(ost); sha1_compress(ost, w);
+    }
+    uint32_t key[8];
+#pragma unroll
+    for (int blkno = 1; blkno <= 2; blkno++) {
+        uint32_t u[5], t[5];
+        {
+            uint32_t w[16] = {p.salt[0], p.salt[1], p.salt[2], p.salt[3], (uint32_t)blkno, 0x80000000u,
+                              0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
+            uint32_t s[5] = {ist[0], ist[1], ist[2], ist[3], ist[4]};
+            sha1_compress(s, w);
+            uint32_t w2[16] = {s[0], s[1], s[2], s[3], s[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
+            u[0] = ost[0]; u[1] = ost[1]; u[2] = ost[2]; u[3] = ost[3]; u[4] = ost[4];
+            sha1_compress(u, w2);
+        }
+        t[0] = u[0]; t[1] = u[1]; t[2] = u[2]; t[3] = u[3]; t[4] = u[4];
+        for (int it = 1; it < 1024; it++) {
+            uint32_t w[16] = {u[0], u[1], u[2], u[3], u[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
+            uint32_t s[5] = {ist[0], ist[1], ist[2], ist[3], ist[4]};
+            sha1_compress(s, w);
+            uint32_t w2[16] = {s[0], s[1], s[2], s[3], s[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
+            u[0] = ost[0]; u[1] = ost[1]; u[2] = ost[2]; u[3] = ost[3]; u[4] = ost[4];
+            sha1_compress(u, w2);
+            t[0] ^= u[0]; t[1] ^= u[1]; t[2] ^= u[2]; t[3] ^= u[3]; t[4] ^= u[4];
+        }
+        if (blkno == 1) { key[0] = t[0]; key[1] = t[1]; key[2] = t[2]; key[3] = t[3]; key[4] = t[4]; }
+        else { key[5] = t[0]; key[6] = t[1]; key[7] = t[2]; }
+    }
+    /* AES-256-CBC decrypt, no padding (:90-92) */
+    uint32_t rk[60], dk[60];
+    aes256_expand(L, key, rk);
+    aes_dec_schedule<14>(L, rk, dk);
+    bool ok;
+    if (p.enc_len == 16u) {
+        /* experimental 2-byte check (:98-101) */
+        uint32_t ct[4] = {p.enc[0], p.enc[1], p.enc[2], p.enc[3]}, pt[4];
+        aes_decrypt<14>(L, dk, ct, pt);
+        ok = ((pt[0] ^ p.iv[0]) >> 16) == 0x0300u;
+    } else {
+        /* SHA256 over the first min(len,1024) plaintext bytes == checksum (:104-123) */
+        uint32_t st[8];
+        sha256_iv(st);
+        uint32_t prev[4] = {p.iv[0], p.iv[1], p.iv[2], p.iv[3]};
+        const uint32_t n = p.hash_len, nfull = n >> 6, rem = n & 63u;
+        for (uint32_t b = 0; b < nfull; b++) {
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t *cp = p.enc + (b * 4u + q) * 4u;
+                uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
+                aes_decrypt<14>(L, dk, ct, pt);
+#pragma unroll
+                for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
+            }
+            sha256_compress(st, w);
+        }
+        /* final block: rem (0/16/32/48) data bytes, 0x80, bit length */
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            if ((uint32_t)q < (rem >> 4)) {
+                const uint32_t *cp = p.enc + (nfull * 4u + q) * 4u;
+                uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
+                aes_decrypt<14>(L, dk, ct, pt);
+#pragma unroll
+                for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) w[4 * q + k] = 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 12; k < 16; k++) w[k] = 0u;
+#pragma unroll
+        for (int k = 0; k < 16; k++) if ((uint32_t)k == (rem >> 2)) w[k] = 0x80000000u;
+        w[15] = n * 8u;
+        sha256_compress(st, w);
+        ok = true;
+#pragma unroll
+        for (int k = 0; k < 8; k++) ok = ok && st[k] == p.checksum[k];
+    }
+    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+    count_block(e, R);
+}
+
+/* ================================================================== PDF R5 (one SHA-256) */
+template <int MODE>
+__global__ void __launch_bounds__(256)
+k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
+    __shared__ uint8_t cs[256];
+    __shared__ uint32_t flag;
+    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
+    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g0 < e.count;
+    const uint32_t g = valid ? g0 : e.count - 1;
+    cand c;
+    get_candidate<MODE, false>(e, cs, g, c);
+    /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
+    uint32_t m[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) m[j] = j < DPRF_SLOT_WORDS ? (c.w[j] & le_keep_mask(j, c.len)) : 0u;
+    /* append the 8 validation-salt bytes (LE words p.u[8], p.u[9]) at byte offset len, then 0x80 */
+    const uint32_t sw[3] = {p.u[8], p.u[9], 0x80u};
+    const uint32_t q = c.len >> 2, r = (c.len & 3u) * 8u;
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+        const uint32_t lo = r ? (sw[s] << r) : sw[s];
+        const uint32_t hi = r ? (sw[s] >> (32u - r)) : 0u;
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            if ((uint32_t)j == q + s) m[j] |= lo;
+            if ((uint32_t)j == q + s + 1) m[j] |= hi;
+        }
+    }
+    /* 0x80 was appended as a byte after the salt: keep only its low byte contribution */
+#pragma unroll
+    for (int j = 0; j < 32; j++) m[j] = bswap32(m[j]);
+    uint32_t hh[8];
+    sha256_msg2(m, c.len + 8u, hh);
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 8; k++) ok = ok && hh[k] == p.u[k];
+    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+    count_block(e, R);
+}
+
+/* ================================================================== PDF R2..R4 (MD5 + RC4) */
+/* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
+ * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave
+ * therefore never conflict, whatever i/j each lane holds. */
+#define RC4_WAVE_BYTES 16384
+DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
+    return ((__builtin_amdgcn_ubfe(j, 2, 6)) << 8) | (j & 3u) | lanebase;
+}
+DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
+DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
+
+/* KSA with an NK-byte key held LE-packed in k[4]. */
+template <int NK>
+DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
+#pragma unroll
+    for (int w = 0; w < 64; w++) *(uint32_t *)(S + (w << 8) + lanebase) = 0x03020100u + 0x04040404u * (uint32_t)w;
+    uint32_t j = 0;
+#pragma unroll
+    for (int i = 0; i < 256; i++) {
+        const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
+        const uint32_t si = lds_ld8(S, ai);
+        const int kb = i % NK;
+        const uint32_t kv = (k[kb >> 2] >> (8 * (kb & 3))) & 0xffu;
+        j = j + si + kv;
+        const uint32_t aj = rc4_addr(j, lanebase);
+        const uint32_t sj = lds_ld8(S, aj);
+        lds_st8(S, ai, sj);
+        lds_st8(S, aj, si);
+    }
+}
+/* PRGA of NB bytes XORed into d[] (LE-packed). */
+template <int NB>
+DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[NB / 4]) {
+    uint32_t j = 0;
+#pragma unroll
+    for (int i = 1; i <= NB; i++) {
+        const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
+        const uint32_t si = lds_ld8(S, ai);
+        j = j + si;
+        const uint32_t aj = rc4_addr(j, lanebase);
+        const uint32_t sj = lds_ld8(S, aj);
+        lds_st8(S, ai, sj);
+        lds_st8(S, aj, si);
+        const uint32_t ks = lds_ld8(S, rc4_addr(si + sj, lanebase));
+        d[(i - 1) >> 2] ^= ks << (8 * ((i - 1) & 3));
+    }
+}
+
+template <int MODE, int R, int NK>
+__global__ void __launch_bounds__(64)
+k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
+    __shared__ uint8_t cs[256];
+    __shared__ uint32_t flag;
+    __shared__ uint32_t padw[16];                 /* PAD || PAD bytes for the runtime-offset padding */
+    __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
+    if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
+    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, &flag)) return;
+    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g0 < e.count;
+    const uint32_t g = valid ? g0 : e.count - 1;
+    cand c;
+    get_candidate<MODE, false>(e, cs, g, c);
+    const uint32_t lanebase = (threadIdx.x & 63u) << 2;
+
+    /* padded password pw[:32] || PAD[0:32-len] (pdf...c:136-139), LE words */
+    const uint32_t len = c.len > 32u ? 32u : c.len;
+    uint32_t pw[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t v = c.w[j] & le_keep_mask(j, len);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t k = 4u * j + b;
+            if (k >= len) v |= (uint32_t)((const uint8_t *)padw)[k - len] << (8 * b);
+        }
+        pw[j] = v;
+    }
+    /* initial hash MD5(padded || O || LE32(P) || ID [|| FFFFFFFF]) (:352-402) */
+    uint32_t h[4];
+    {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { m[j] = pw[j]; m[8 + j] = p.tail[j]; }
+        md5_iv(h);
+        md5_compress(h, m);
+        for (uint32_t b = 0; b < p.tail_blocks; b++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) m[j] = p.tail[8 + 16 * b + j];
+            md5_compress(h, m);
+        }
+    }
+    if (R >= 3) {
+        /* 50 x MD5(h[0:n]) (:150-155) */
+        for (int i = 0; i < 50; i++) {
+            uint32_t m[16];
+            if (NK == 16) {
+                m[0] = h[0]; m[1] = h[1]; m[2] = h[2]; m[3] = h[3]; m[4] = 0x80u;
+#pragma unroll
+                for (int j = 5; j < 16; j++) m[j] = 0u;
+                m[14] = 128u;
+            } else {
+                m[0] = h[0]; m[1] = (h[1] & 0xffu) | 0x8000u;
+#pragma unroll
+                for (int j = 2; j < 16; j++) m[j] = 0u;
+                m[14] = 40u;
+            }
+            md5_iv(h);
+            md5_compress(h, m);
+        }
+    }
+    uint8_t *Sw = S;   /* one wave per block: the whole array is this wave's */
+    bool ok;
+    if (R == 2) {
+        /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189) */
+        uint32_t d[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) d[j] = p.pad[j];
+        rc4_ksa<5>(Sw, lanebase, h);
+        rc4_prga<32>(Sw, lanebase, d);
+        ok = true;
+#pragma unroll
+        for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
+    } else {
+        /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
+        uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
+        for (uint32_t x = 0; x < 20u; x++) {
+            const uint32_t xx = x * 0x01010101u;
+            uint32_t k[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
+            rc4_ksa<NK>(Sw, lanebase, k);
+            rc4_prga<16>(Sw, lanebase, d);
+        }
+        ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
+    }
+    if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
+    count_block(e, R_);
+}
+
+/* ------------------------------------------------------------------ launchers */
+#define GRID(n, b) dim3(((n) + (b) - 1) / (b))
+
+hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
+    if (e.mode == 0) hipLaunchKernelGGL(k_office<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+    else hipLaunchKernelGGL(k_office<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+    return hipGetLastError();
+}
+hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
+                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
+    if (e.mode == 0) hipLaunchKernelGGL(k_odt<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+    else hipLaunchKernelGGL(k_odt<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+    return hipGetLastError();
+}
+hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
+                         uint32_t stop, hipStream_t s) {
+    if (e.mode == 0) hipLaunchKernelGGL(k_pdf_r5<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, cap, stop);
+    else hipLaunchKernelGGL(k_pdf_r5<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, cap, stop);
+    return hipGetLastError();
+}
+hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
+                          uint32_t stop, hipStream_t s) {
+#define L24(M, RR, NK) hipLaunchKernelGGL((k_pdf_r24<M, RR, NK>), GRID(e.count, 64), dim3(64), 0, s, e, p, R, cap, stop)
+    if (p.R == 2) { if (e.mode == 0) L24(0, 2, 5); else L24(1, 2, 5); }
+    else if (p.n == 16) { if (e.mode == 0) L24(0, 3, 16); else L24(1, 3, 16); }
+    else { if (e.mode == 0) L24(0, 3, 5); else L24(1, 3, 5); }
+#undef L24
+    return hipGetLastError();
+}

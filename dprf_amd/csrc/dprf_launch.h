@@ -1,0 +1,17 @@
+/* dprf_launch.h -- host-side launchers of the verification kernels (internal to libdprf.so). */
+#ifndef DPRF_LAUNCH_H
+#define DPRF_LAUNCH_H
+#include <hip/hip_runtime.h>
+#include "dprf_params.h"
+
+hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s);
+hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
+                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s);
+hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
+                         uint32_t stop, hipStream_t s);
+hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
+                          uint32_t stop, hipStream_t s);
+hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s);
+#endif

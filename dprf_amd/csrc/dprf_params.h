@@ -1,0 +1,78 @@
+/* dprf_params.h -- kernel-argument structs shared by the host (dprf_host.cpp) and the gfx950 kernels
+ * (dprf_kernels.hip).  Plain C layout; everything a kernel needs about one document is folded here
+ * once per context, never per candidate.  Word conventions: "BE" = the 32-bit big-endian words that
+ * SHA-1/SHA-2/AES operate on; "LE" = little-endian words (MD5, RC4 byte order, candidate bytes). */
+#ifndef DPRF_PARAMS_H
+#define DPRF_PARAMS_H
+#include <stdint.h>
+
+#define DPRF_SLOT_WORDS 16          /* list-mode candidate slot: 64 bytes, LE-packed */
+#define DPRF_MAX_RANGE_LEN 32
+
+/* Candidate source for one launch.  Range mode: candidate g of the launch is global keyspace index
+ * start + g, spelled over charset in itertools.product order.  List mode: candidate g is slot
+ * start + g of the device candidate buffer. */
+struct dprf_enum {
+    uint64_t start;
+    uint32_t count;
+    uint32_t mode;                  /* 0 range, 1 list */
+    uint32_t pwlen;                 /* range: fixed length (bytes) */
+    uint32_t cslen;
+    uint32_t div_m;                 /* u32 division by cslen: q = (mulhi(n,m) + ((n-mulhi)>>1)) >> s */
+    uint32_t div_s;
+    uint8_t sdig[DPRF_MAX_RANGE_LEN];   /* base-cslen digits of start, most significant first */
+    uint8_t charset[256];
+    const uint32_t *slots;          /* list: [n][DPRF_SLOT_WORDS] LE words */
+    const uint8_t *lens;            /* list: [n] byte lengths */
+};
+
+/* Device results of one API call (accumulated over its launches). */
+struct dprf_results {
+    uint32_t nhits;                 /* total hits (may exceed cap) */
+    uint32_t stop;                  /* set by a hit when stop_on_first */
+    unsigned long long first;       /* lowest hit index (atomicMin), ~0 if none */
+    unsigned long long evaluated;   /* candidates evaluated (per-block atomicAdd) */
+    unsigned long long hits[1];     /* [cap] */
+};
+
+/* AES tables, generated on the host from the GF(2^8) definition (FIPS 197 5.1.1) and copied to LDS by
+ * each kernel that needs them. */
+struct dprf_aes_tables {
+    uint32_t te0[256];              /* forward T-table, BE column (S[x]*{02,01,01,03}) */
+    uint32_t td0[256];              /* inverse T-table, BE column (Si[x]*{0e,09,0d,0b}) */
+    uint8_t sbox[256];
+    uint8_t inv_sbox[256];
+};
+
+/* Office: msoffcrypto_password_verifier.c:56-191 */
+struct dprf_office_params {
+    uint32_t salt[4];               /* BE words of salt[0:16] (:95) */
+    uint32_t ev[4];                 /* encrypted verifier, BE */
+    uint32_t evh[8];                /* encrypted verifier hash (32 B), BE */
+    uint32_t hash_size;             /* byte of dec(evh) that must be 0 (:168) */
+};
+
+/* ODT: odt_password_verifier.c:51-126 */
+struct dprf_odt_params {
+    uint32_t checksum[8];           /* BE */
+    uint32_t iv[4];                 /* BE */
+    uint32_t salt[4];               /* BE */
+    uint32_t enc_len;               /* bytes; multiple of 16 */
+    uint32_t hash_len;              /* min(enc_len, 1024) */
+    const uint32_t *enc;            /* device: first hash_len bytes of ciphertext, BE words */
+};
+
+/* PDF: pdf_password_verifier.c:64-291 */
+#define DPRF_PDF_TAIL_WORDS 64
+struct dprf_pdf_params {
+    uint32_t R;                     /* 2..6 */
+    uint32_t n;                     /* Length / 8 (R<=4) */
+    uint32_t u[12];                 /* R<=4: U[0:32] LE words; R5/R6: U[0:32] BE words + salt BE */
+    uint32_t h2[4];                 /* R3/R4: MD5(PAD || ID), LE (pdf...c:167) */
+    uint32_t pad[8];                /* the 32-byte password padding, LE */
+    uint32_t tail_blocks;           /* MD5 blocks after the first (initial hash, :352-402) */
+    uint32_t tail[DPRF_PDF_TAIL_WORDS]; /* LE words of O||LE32(P)||ID[||FFFFFFFF] + MD5 padding,
+                                           starting at message byte 32 */
+};
+
+#endif

@@ -1,0 +1,102 @@
+/* dprf.h -- C ABI of libdprf.so, the MI355X (gfx950) brute-force verification engine.
+ *
+ * Drop-in boundary.  The reference engine (/root/reference/src/brute_force.py) verifies one candidate
+ * per OS process: _brute_force() (brute_force.py:106-161) Popen()s one of three verifier executables
+ * per password (_call_msoffcrypto_core :163-173, _call_odt_core :175-182, _call_pdf_core :184-197)
+ * whose exit code is verify()'s verdict (msoffcrypto_password_verifier.c:52, odt_password_verifier.c:47,
+ * pdf_password_verifier.c:60).  This library replaces that inner loop, the three executables and the
+ * OpenSSL arithmetic under them with batched gfx950 kernels, one candidate per lane.
+ *
+ * Plain C types only; no torch or HIP types cross the boundary.  Every call returns DPRF_OK (0) or a
+ * negative DPRF_E_* code and sets a thread-local message readable with dprf_last_error().  An error is
+ * never reported as "found" (the reference conflates the two: any non-zero exit counts as a hit,
+ * brute_force.py:140).
+ *
+ * Threading: a context is bound to one device and owns one HIP stream; calls on DIFFERENT contexts may
+ * run concurrently from different threads; calls on the SAME context must be serialised by the caller.
+ * Ownership: the caller owns every buffer it passes; they are read/written only during the call.
+ */
+#ifndef DPRF_H
+#define DPRF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPRF_ABI_VERSION 1
+
+/* formats: the tag parse_verification_data extracts (brute_force.py:250) */
+#define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
+#define DPRF_FMT_ODT 2      /* "$odt$*1.2*..."      ODF 1.2 AES-256-CBC / PBKDF2-HMAC-SHA1     */
+#define DPRF_FMT_PDF 3      /* "$pdf$*V*R*..."      PDF standard security handler R2..R6       */
+
+/* error codes */
+#define DPRF_OK 0
+#define DPRF_E_INVALID (-1)      /* bad argument / malformed field array                          */
+#define DPRF_E_DOMAIN (-2)       /* stream outside the parity domain: the reference's behaviour is
+                                    undefined or an abort() there           */
+#define DPRF_E_HIP (-3)          /* HIP runtime error (message has the hipError string)           */
+#define DPRF_E_NODEVICE (-4)     /* no usable gfx950 device / bad device ordinal                  */
+#define DPRF_E_PWLEN (-5)        /* candidate longer than the kernel supports (see DPRF_MAX_PW)    */
+#define DPRF_E_CHARSET (-6)      /* charset invalid for this format (e.g. non-ASCII for Office)    */
+
+/* context flags (dprf_ctx_flags) */
+#define DPRF_FLAG_NEVER_MATCHES 1        /* reference verify() returns 0 for every candidate: (V,R)
+                                            gate / Length%8 (pdf...c:89-101), ev/evh length (office
+                                            ...c:163,168).  Searches still run and find nothing.   */
+#define DPRF_FLAG_REF_NONDETERMINISTIC 2 /* a hex field starts with 00: the reference's str_to_uchar
+                                            (BN_hex2bn/BN_bn2bin) decodes it short and reads
+                                            uninitialised bytes; this library decodes it in full.   */
+
+/* Longest candidate the kernels accept, in bytes of the password as given (UTF-8).  Office counts
+ * UTF-16 code units instead (<= 32).  PDF R2-R4 truncate at 32 bytes like the reference
+ * (pdf...c:137), so longer candidates are accepted there. */
+#define DPRF_MAX_PW 64
+#define DPRF_MAX_PW_RANGE 32   /* longest fixed length for dprf_search_range */
+
+typedef struct dprf_ctx dprf_ctx;
+
+typedef struct dprf_stats {
+    uint64_t candidates;   /* candidates fully evaluated on the device                          */
+    uint64_t launches;     /* verification-kernel launches                                      */
+    double kernel_ms;      /* sum of HIP-event durations of those launches (on the ctx stream)  */
+    double wall_ms;        /* host wall time of the call, first launch to last result copy      */
+    uint32_t stopped_early;/* 1 if stop_on_first ended the search before the whole range        */
+    uint32_t reserved;
+} dprf_stats;
+
+/* ---- library ---- */
+int dprf_abi_version(void);
+const char *dprf_last_error(void);
+int dprf_device_count(void);      /* gfx950 devices visible to this process */
+
+/* ---- context: one document, one device ----
+ * fields/nfields: the array parse_verification_data() returns (brute_force.py:245-264), i.e. the
+ * stream split on '*' with fields[0] replaced by the format tag ("office", "odt" or "pdf"); office
+ * needs 8 fields, odt 7, pdf 12.  The per-format field meaning is exactly the reference's argv mapping
+ * (brute_force.py:163-197).  device: HIP device ordinal. */
+int dprf_ctx_create(const char *const *fields, int nfields, int device, dprf_ctx **out);
+int dprf_ctx_destroy(dprf_ctx *ctx);
+int dprf_ctx_format(const dprf_ctx *ctx);
+int dprf_ctx_flags(const dprf_ctx *ctx);
+const char *dprf_ctx_kernel(const dprf_ctx *ctx);   /* kernel family name, e.g. "pdf_r34" */
+
+/* ---- range mode: brute_force.py -pr N (init_rangebased_brute_force :60-79, _generate :199-219) ----
+ * Verifies candidates [start, start+count) of charset^pwlen in itertools.product order (leftmost
+ * character most significant).  Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total
+ * number of hits found (may exceed cap).  stop_on_first != 0 stops after the launch containing the
+ * lowest hit, which is then hits[0].  stats may be NULL. */
+int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwlen, uint64_t start,
+                      uint64_t count, int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits,
+                      dprf_stats *stats);
+
+/* ---- list mode: client payloads (init_listbased_brute_force :82-104, client.py:105) ----
+ * Candidate k is blob[offsets[k] .. offsets[k+1]) (n+1 offsets).  Hits are list indices. */
+int dprf_verify_list(dprf_ctx *ctx, const uint8_t *blob, const uint64_t *offsets, int64_t n,
+                     int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

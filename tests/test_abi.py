@@ -1,0 +1,55 @@
+"""The C-ABI library loads and exports every symbol include/dprf.h declares (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def declared_symbols():
+    hdr = open(os.path.join(REPO, "include", "dprf.h")).read()
+    return sorted(set(re.findall(r"\b(dprf_[a-z_]+)\s*\(", hdr)))
+
+
+def test_header_and_python_binding_agree():
+    from dprf_amd import _lib
+    assert declared_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    from dprf_amd import _lib
+    L = _lib.lib()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+    assert L.dprf_abi_version() == _lib.ABI_VERSION
+
+
+def test_constants_match_header():
+    from dprf_amd import _lib
+    hdr = open(os.path.join(REPO, "include", "dprf.h")).read()
+    consts = dict((k, int(v)) for k, v in re.findall(r"#define (DPRF_\w+) \(?(-?\d+)\)?", hdr))
+    assert consts["DPRF_ABI_VERSION"] == _lib.ABI_VERSION
+    assert consts["DPRF_E_DOMAIN"] == _lib.E_DOMAIN and consts["DPRF_E_NODEVICE"] == _lib.E_NODEVICE
+    assert consts["DPRF_MAX_PW"] == _lib.MAX_PW and consts["DPRF_MAX_PW_RANGE"] == _lib.MAX_PW_RANGE
+    assert consts["DPRF_FLAG_NEVER_MATCHES"] == _lib.FLAG_NEVER_MATCHES
+
+
+def test_no_device_is_an_error_not_a_fallback():
+    """Without a GPU, creating a context must fail loudly (DPRF_E_NODEVICE) -- there is no CPU path."""
+    from dprf_amd import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(_lib.DprfError) as ei:
+        _lib.Context(["pdf", "1", "2", "40", "-64", "1", "16", "11" * 16, "32", "22" * 32, "32", "33" * 32])
+    assert ei.value.code == _lib.E_NODEVICE
+
+
+def test_product_does_not_import_the_oracle():
+    """Nothing under dprf_amd/ may import, load or execute oracle/ (it is the checker)."""
+    for root, _, files in os.walk(os.path.join(REPO, "dprf_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                src = open(os.path.join(root, f), errors="replace").read()
+                assert "pyoracle" not in src and "liboracle" not in src and "oracle.h" not in src, f

@@ -1,0 +1,203 @@
+"""GPU parity: libdprf.so's kernels vs the reference's verdicts (golden fixtures) and vs the oracle, through
+the C ABI.  Bit-exact: hit sets must be identical."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOWER = "abcdefghijklmnopqrstuvwxyz"
+ALNUM = LOWER + LOWER.upper() + "0123456789"
+
+
+@pytest.fixture(scope="module")
+def dprf():
+    from dprf_amd import _lib
+    assert _lib.device_count() >= 1, "no gfx950 device: GPU tests need the MI355X box"
+    return _lib
+
+
+def ctx_for(dprf, streams, name):
+    from dprf_amd import brute_force as bf
+    return dprf.Context(bf.parse_verification_data(streams[name]["stream"]))
+
+
+def test_kernel_families(dprf, streams):
+    want = {"office": "office_std", "odt": "odf_aes256"}
+    for name in streams:
+        c = ctx_for(dprf, streams, name)
+        fam = c.kernel
+        if name.startswith("pdf"):
+            assert fam.startswith("pdf_r"), (name, fam)
+        else:
+            assert fam == want[name.split("_")[0]], (name, fam)
+
+
+def test_verdict_tables_match_reference(dprf, streams, verdicts):
+    for name, table in verdicts.items():
+        c = ctx_for(dprf, streams, name)
+        cands = [p for p, _ in table]
+        hits, n, st = c.verify_list(cands)
+        want = [i for i, (_, v) in enumerate(table) if v]
+        assert hits == want, (name, [cands[i] for i in hits], [cands[i] for i in want])
+        assert st["candidates"] == len(cands)
+
+
+def test_hitsets_match_reference(dprf, streams, hitsets):
+    for key, h in hitsets.items():
+        c = ctx_for(dprf, streams, h["stream"])
+        hits, n, st = c.search_range(h["charset"], h["pwlen"], h["start"], h["count"])
+        assert hits == h["hits"] and n == len(h["hits"]), key
+        assert st["candidates"] == h["count"], key
+
+
+def test_every_stream_finds_its_password_in_range_mode(dprf, streams):
+    for name, d in streams.items():
+        pw = d["password"]
+        if len(pw) > 4 or any(ch not in ALNUM for ch in pw):
+            continue
+        cs = LOWER if all(ch in LOWER for ch in pw) else ALNUM
+        idx = 0
+        for ch in pw:
+            idx = idx * len(cs) + cs.index(ch)
+        c = ctx_for(dprf, streams, name)
+        lo = max(0, idx - 3000)
+        hits, n, _ = c.search_range(cs, len(pw), lo, min(6000, len(cs) ** len(pw) - lo))
+        assert idx in hits, name
+
+
+def _random_words(rng, n, lo=1, hi=12, alphabet=ALNUM):
+    return ["".join(rng.choice(alphabet) for _ in range(rng.randint(lo, hi))) for _ in range(n)]
+
+
+@pytest.mark.parametrize("name,n", [("pdf_testdoc_r2", 3000), ("pdf_testdoc_r4", 3000), ("pdf_synth_r3_l40_cab", 3000),
+                                    ("pdf_synth_r4_meta0_dog", 3000), ("pdf_synth_r5_cat", 3000),
+                                    ("pdf_synth_r6_ox", 150), ("odt_testdoc_e", 800), ("odt_testdoc_std", 400),
+                                    ("office_testdoc", 24)])
+def test_random_lists_vs_oracle(dprf, oracle, streams, name, n):
+    rng = random.Random(hash(name) & 0xffff)
+    words = _random_words(rng, n) + [streams[name]["password"]]
+    rng.shuffle(words)
+    want = [i for i, v in enumerate(oracle.Ctx(streams[name]["stream"]).verify_list(words)) if v == 1]
+    hits, _, _ = ctx_for(dprf, streams, name).verify_list(words)
+    assert hits == want
+
+
+@pytest.mark.parametrize("name", ["pdf_synth_r2_key", "pdf_synth_r3_l128_abc", "pdf_synth_r5_cat", "pdf_synth_r6_ox",
+                                  "odt_synth_std_zq", "office_synth_ok"])
+def test_ragged_lengths_and_limits(dprf, oracle, streams, name):
+    """Lengths 0..64 in one payload (32/33 around the PDF truncation, 55/56 around the SHA block edge)."""
+    rng = random.Random(11)
+    lens = list(range(0, 65)) if not name.startswith("office") else [1, 2, 19, 20, 27, 28, 31, 32]
+    words = ["".join(rng.choice(ALNUM) for _ in range(k)) for k in lens] + [streams[name]["password"]]
+    if name.startswith("office"):
+        words = [w for w in words if w]
+    want = [i for i, v in enumerate(oracle.Ctx(streams[name]["stream"]).verify_list(words)) if v == 1]
+    hits, _, st = ctx_for(dprf, streams, name).verify_list(words)
+    assert hits == want
+    assert st["candidates"] == len(words)
+
+
+def test_pdf_truncates_long_candidates_like_reference(dprf, oracle, streams):
+    """R<=4 only looks at the first 32 bytes (pdf_password_verifier.c:137): candidates sharing a 32-byte
+    prefix get the same verdict."""
+    words = ["Q" * 32, "Q" * 33, "Q" * 40, "Q" * 64, "Q" * 31]
+    want = [v for v in oracle.Ctx(streams["pdf_testdoc_r4"]["stream"]).verify_list(words)]
+    hits, _, _ = ctx_for(dprf, streams, "pdf_testdoc_r4").verify_list(words)
+    assert hits == [i for i, v in enumerate(want) if v == 1]
+
+
+def test_office_utf8_candidates(dprf, oracle, streams):
+    words = ["été", "passwörd", "ok", "日本語", "😀ok", "o", "k"]
+    want = [i for i, v in enumerate(oracle.Ctx(streams["office_synth_ok"]["stream"]).verify_list(words)) if v == 1]
+    hits, _, _ = ctx_for(dprf, streams, "office_synth_ok").verify_list(words)
+    assert hits == want == [2]
+
+
+def test_errors_are_errors_not_hits(dprf, streams):
+    c = ctx_for(dprf, streams, "office_synth_ok")
+    with pytest.raises(dprf.DprfError) as ei:
+        c.verify_list([""])
+    assert ei.value.code == dprf.E_DOMAIN
+    with pytest.raises(dprf.DprfError) as ei:
+        c.verify_list([b"\xff\xfe"])
+    assert ei.value.code == dprf.E_DOMAIN
+    with pytest.raises(dprf.DprfError) as ei:
+        c.search_range("aé", 2, 0, 4)
+    assert ei.value.code == dprf.E_CHARSET
+    c2 = ctx_for(dprf, streams, "pdf_synth_r6_ox")
+    with pytest.raises(dprf.DprfError) as ei:
+        c2.verify_list(["x" * 65])
+    assert ei.value.code == dprf.E_PWLEN
+    with pytest.raises(dprf.DprfError):
+        c2.search_range(LOWER, 3, 26 ** 3 - 5, 10)
+
+
+def test_never_matches_and_empty_inputs(dprf):
+    f = ["pdf", "2", "4", "128", "-4", "1", "16", "11" * 16, "32", "22" * 32, "32", "33" * 32]
+    c = dprf.Context(f)
+    assert c.flags & dprf.FLAG_NEVER_MATCHES
+    hits, n, st = c.search_range(LOWER, 3, 0, 26 ** 3)
+    assert hits == [] and n == 0 and st["candidates"] == 26 ** 3
+    c2 = dprf.Context(["pdf", "1", "2", "40", "-64", "1", "16", "11" * 16, "32", "22" * 32, "32", "33" * 32])
+    assert c2.verify_list([]) == ([], 0, c2.verify_list([])[2])
+    assert c2.search_range(LOWER, 2, 0, 0)[1] == 0
+
+
+def test_domain_streams_rejected(dprf):
+    with pytest.raises(dprf.DprfError) as ei:
+        dprf.Context(["odt", "1.2", "11" * 32, "22" * 16, "33" * 16, "44" * 17, "17"])
+    assert ei.value.code == dprf.E_DOMAIN
+    with pytest.raises(dprf.DprfError) as ei:
+        dprf.Context(["pdf", "2", "3", "64", "-4", "1", "16", "11" * 16, "32", "22" * 32, "32", "33" * 32])
+    assert ei.value.code == dprf.E_DOMAIN
+
+
+def test_many_hits_overflow_and_order(dprf, streams, hitsets):
+    """The ODT -e 2-byte check has ~2^-16 false positives: a 26^4 scan has 10 (reference, Appendix A)."""
+    key = "odt_testdoc_e/lower^4"
+    if key not in hitsets:
+        pytest.skip("slow golden scan not generated")
+    c = ctx_for(dprf, streams, "odt_testdoc_e")
+    hits, n, _ = c.search_range(LOWER, 4, 0, 26 ** 4)
+    assert hits == hitsets[key]["hits"] and n == 10
+    hits3, n3, _ = c.search_range(LOWER, 4, 0, 26 ** 4, cap=3)
+    assert n3 == 10 and hits3 == hitsets[key]["hits"][:3]
+
+
+def test_stop_on_first_returns_lowest(dprf, streams):
+    c = ctx_for(dprf, streams, "odt_testdoc_e")
+    hits, n, st = c.search_range(LOWER, 4, 0, 26 ** 4, stop_on_first=True, cap=1)
+    assert hits == [27692]
+
+
+def test_range_split_consistency(dprf, streams):
+    """A keyspace scanned in one call == the same keyspace scanned in ragged pieces (chunk seams)."""
+    c = ctx_for(dprf, streams, "pdf_synth_r4_alnum")
+    total = 62 ** 3
+    whole, n, _ = c.search_range(ALNUM, 3, 0, total)
+    pieces, s = [], 0
+    for step in [1, 7, 4095, 100000, total]:
+        k = min(step, total - s)
+        if k <= 0:
+            break
+        pieces += c.search_range(ALNUM, 3, s, k)[0]
+        s += k
+    assert s == total and pieces == whole and len(whole) >= 1
+
+
+def test_list_mode_equals_range_mode(dprf, streams):
+    from dprf_amd import brute_force as bf
+    c = ctx_for(dprf, streams, "pdf_synth_r5_alnum")
+    start, count = 62 ** 3 - 20000, 20000
+    rng_hits, _, _ = c.search_range(ALNUM, 3, start, count)
+    words = [bf._index_to_password(start + i, ALNUM, 3) for i in range(count)]
+    lst_hits, _, _ = c.verify_list(words)
+    assert [start + i for i in lst_hits] == rng_hits
+
+
+def test_brute_force_module_end_to_end(dprf, streams):
+    from dprf_amd import brute_force as bf
+    assert bf.init(streams["pdf_synth_r3_l128_abc"]["stream"], 3, None, devices=[0]) == (1, "abc")
+    assert bf.init(streams["pdf_testdoc_r2"]["stream"], 2, None, devices=[0]) == (0, "default_password_allocation")
+    assert bf.init(streams["office_testdoc"]["stream"], 0, ["x", "password", "y"], devices=[0]) == (1, "password")

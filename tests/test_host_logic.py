@@ -1,0 +1,63 @@
+"""Host-side logic of the brute_force counterpart (no GPU): field split, tag regex, argument checks,
+enumeration order, parsers."""
+import itertools
+
+import pytest
+
+from dprf_amd import brute_force as bf
+from dprf_amd.parsers import odt2hashes
+
+
+def test_parse_verification_data_matches_reference_shapes(streams):
+    for name, d in streams.items():
+        f = bf.parse_verification_data(d["stream"])
+        assert f[0] in ("office", "odt", "pdf")
+        assert len(f) == {"office": 8, "odt": 7, "pdf": 12}[f[0]]
+
+
+@pytest.mark.parametrize("bad", ["x:$office$*2007*20", "garbage", "x:$zip$*1*2*3", "x:$pdf$*1*2"])
+def test_unsupported_stream_exits_1(bad):
+    with pytest.raises(SystemExit) as ei:
+        bf.parse_verification_data(bad)
+    assert ei.value.code == 1
+
+
+def test_init_argument_checks():
+    with pytest.raises(ValueError):
+        bf.init("x:$pdf$*", 0, None)
+    with pytest.raises(ValueError):
+        bf.init("x:$pdf$*", 3, ["a"])
+
+
+@pytest.mark.parametrize("cs,n", [("abc", 3), (bf.LOWERCASE, 2), (bf.ALNUM, 2), ("z", 4)])
+def test_index_order_is_itertools_product(cs, n):
+    ref = ["".join(t) for t in itertools.product(cs, repeat=n)]
+    assert [bf._index_to_password(i, cs, n) for i in range(len(ref))] == ref
+
+
+def test_odt_parser_matches_golden(streams):
+    path = "/root/reference/test/files/odt/password.odt"
+    import os
+    if not os.path.exists(path):
+        pytest.skip("reference test document not present")
+    assert odt2hashes.get_hashes(path, True) == streams["odt_testdoc_e"]["stream"]
+    assert odt2hashes.get_hashes(path, False) == streams["odt_testdoc_std"]["stream"]
+
+
+def _fastdiv(n, d):
+    """The u32 division the kernels use (dprf_kernels.hip fastdiv) with the host magic (dprf_host.cpp)."""
+    if d <= 1:
+        return n
+    l = (d - 1).bit_length()
+    m = ((1 << 32) * ((1 << l) - d)) // d + 1
+    t = (n * m) >> 32
+    return (t + ((n - t) >> 1)) >> (l - 1)
+
+
+def test_fastdiv_magic_exact():
+    import random
+    rng = random.Random(7)
+    for d in list(range(1, 257)):
+        for n in [0, 1, d - 1, d, d + 1, 2 ** 32 - 1, 2 ** 31, 2 ** 32 - d] + [rng.getrandbits(32) for _ in range(200)]:
+            n &= 0xffffffff
+            assert _fastdiv(n, d) == n // d, (n, d)

@@ -1,0 +1,105 @@
+"""Pin the CPU restatement (oracle/) against the REFERENCE: every verdict, hit set and -v intermediate in
+tests/golden/ was produced by the reference's own verifier executables (tests/golden/make_golden.py)."""
+import pytest
+
+LOWER = "abcdefghijklmnopqrstuvwxyz"
+
+
+def test_every_stream_accepts_its_password(oracle, streams):
+    for name, d in streams.items():
+        assert oracle.Ctx(d["stream"]).verify(d["password"]) == 1, name
+
+
+def test_verdict_tables_match_reference(oracle, streams, verdicts):
+    for name, table in verdicts.items():
+        ctx = oracle.Ctx(streams[name]["stream"])
+        got = ctx.verify_list([c for c, _ in table])
+        want = [v for _, v in table]
+        assert got == want, (name, [(c, g, w) for (c, w), g in zip(table, got) if g != w])
+
+
+def test_hitsets_match_reference(oracle, streams, hitsets):
+    for key, h in hitsets.items():
+        if h["count"] > 20000 and streams[h["stream"]]["stream"].find("$odt$") >= 0:
+            continue                      # the [a-z]^4 ODT scan is covered on the GPU
+        ctx = oracle.Ctx(streams[h["stream"]]["stream"])
+        hits, n = ctx.search_range(h["charset"], h["pwlen"], h["start"], h["count"])
+        assert hits == h["hits"], key
+
+
+def _lines(inter, name):
+    return inter[name]["lines"]
+
+
+def test_office_intermediates_match_reference_v_output(oracle, streams, intermediates):
+    for name in ("office_testdoc", "office_synth_ok", "office_synth_dprf"):
+        d = streams[name]
+        got = oracle.Ctx(d["stream"]).intermediates(d["password"])
+        L = _lines(intermediates, name)
+        assert got[0:20].hex() == L["Final hash"]
+        assert got[20:40].hex() == L["X1"]
+        assert got[40:56].hex() == L["Derived key"]
+        assert got[56:76].hex() == L["Decrypted 'EncryptedVerifier' hash"]
+
+
+def test_odt_intermediates_match_reference_v_output(oracle, streams, intermediates):
+    for name in ("odt_testdoc_e", "odt_testdoc_std", "odt_synth_std_zq"):
+        d = streams[name]
+        got = oracle.Ctx(d["stream"]).intermediates(d["password"])
+        L = _lines(intermediates, name)
+        assert got[0:32].hex() == L["Starting key"]
+        assert got[32:64].hex() == L["Derived key"]
+
+
+def test_pdf_intermediates_match_reference_v_output(oracle, streams, intermediates):
+    for name, d in streams.items():
+        if not name.startswith("pdf"):
+            continue
+        f = oracle.split_stream(d["stream"])
+        got = oracle.Ctx(d["stream"]).intermediates(d["password"])
+        L = _lines(intermediates, name)
+        R = int(f[2])
+        if R <= 4:
+            assert got[0:32].hex() == L["Padded password"], name
+            n = int(f[3]) // 8
+            assert got[32:32 + n].hex() == L["Initial hash"], name
+            assert got[48:80].hex() == L["Actual U value"], name
+        else:
+            assert got[0:32].hex() == L["Computed hash"], name
+
+
+def test_appendix_a_office_vectors(oracle, streams):
+    got = oracle.Ctx(streams["office_testdoc"]["stream"]).intermediates("password")
+    assert got[0:20].hex() == "d3d76b62771e7b1a6c5d2dc2bb30ac4cf9cf037a"
+    assert got[20:40].hex() == "38dc4cb3cdd294ebdc62e5aed5f6775daf2b7810"
+
+
+def test_work_counts_office(oracle, streams):
+    c = oracle.Ctx(streams["office_testdoc"]["stream"]).work_counts("password")
+    assert c["sha1c"] == 1 + 50000 + 1 + 2 + 1
+    assert c["aes128_key_exp"] == 1
+
+
+def test_work_counts_odt(oracle, streams):
+    c = oracle.Ctx(streams["odt_testdoc_std"]["stream"]).work_counts("password")
+    assert c["sha1c"] == 2 + 2 * (2 + 1023 * 2)
+    assert c["aes256_dec_blocks"] == 64
+    assert c["sha256c"] == 1 + 17
+
+
+@pytest.mark.parametrize("bad", [
+    "x:$office$*2007*20*128*16*de40*1895*31c1",                      # lengths not multiples of 16 -> abort
+    "x:$odt$*1.2*" + "11" * 32 + "*" + "22" * 16 + "*" + "33" * 16 + "*" + "44" * 17 + "*17",
+    "x:$pdf$*2*3*64*-4*1*16*" + "11" * 16 + "*32*" + "22" * 32 + "*32*" + "33" * 32,   # R3 with 8-byte key
+])
+def test_outside_parity_domain_is_rejected(oracle, bad):
+    with pytest.raises(ValueError):
+        oracle.Ctx(bad)
+
+
+def test_never_matches_gate(oracle):
+    # (V,R) = (2,4) fails the whitelist (pdf_password_verifier.c:89-96): every candidate verifies 0
+    s = "x:$pdf$*2*4*128*-4*1*16*" + "11" * 16 + "*32*" + "22" * 32 + "*32*" + "33" * 32
+    c = oracle.Ctx(s)
+    assert c.flags & oracle.FLAG_NEVER_MATCHES
+    assert c.verify("anything") == 0
