@@ -140,6 +140,14 @@ def cpu_baseline(fields, charset, pwlen, seconds=1.5, procs=None):
 
 
 # ------------------------------------------------------------------ GPU timing
+def shard(step, rank, world, batch, space):
+    """Keyspace slice of `rank` at `step`: step s covers the contiguous block [s*world*B, (s+1)*world*B)
+    (wrapped inside the keyspace) and rank r takes its r-th B-sized piece -- contiguous shards, no
+    overlap, no gaps, and no data exchange between ranks."""
+    start = ((step * world + rank) * batch) % max(1, space - batch)
+    return start, min(batch, space - start)
+
+
 def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, batch=None):
     _, cs, pwlen, B, _, _ = WORKLOADS[name]
     B = batch or B
@@ -148,8 +156,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
     lowest = None
 
     def step(s):
-        start = ((s * world + rank) * B) % max(1, space - B)
-        hits, n, st = ctx.search_range(cs, pwlen, start, min(B, space - start))
+        start, n = shard(s, rank, world, B, space)
+        hits, _, st = ctx.search_range(cs, pwlen, start, n)
         first = hits[0] if hits else (1 << 62)
         return allreduce_min(first), st
 

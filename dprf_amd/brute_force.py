@@ -94,12 +94,11 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
         found = None
         while done < space and found is None:
             block = min(space - done, ROUND_PER_DEVICE * len(ctxs))
-            per = -(-block // len(ctxs))
+            slices = _round_slices(done, block, len(ctxs))
             results = [None] * len(ctxs)
 
             def work(k):
-                s = done + k * per
-                n = max(0, min(per, done + block - s))
+                s, n = slices[k]
                 results[k] = ctxs[k].search_range(charset, password_range, s, n, stop_on_first=True, cap=1) if n else ([], 0, {})
 
             if len(ctxs) == 1:
@@ -118,6 +117,16 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
     finally:
         for c in ctxs:
             c.close()
+
+
+def _round_slices(done, block, ndev):
+    """Contiguous (start, count) slices, one per device, tiling [done, done + block)."""
+    per = -(-block // ndev)
+    out = []
+    for k in range(ndev):
+        s = done + k * per
+        out.append((min(s, done + block), max(0, min(per, done + block - s))))
+    return out
 
 
 def init_listbased_brute_force(input_data, passwords, devices=None):

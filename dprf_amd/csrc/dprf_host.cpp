@@ -170,6 +170,7 @@ struct dprf_ctx {
     uint32_t *d_enc = nullptr;
     dprf_results *d_res = nullptr;
     uint32_t *d_slots = nullptr;
+    uint32_t *d_keys = nullptr;      /* KDF -> check hand-off, 8 words per candidate of one chunk */
     uint8_t *d_lens = nullptr;
     size_t slot_cap = 0;
     dprf_results *h_hdr = nullptr;   /* pinned copy of the results header */
@@ -298,6 +299,18 @@ static int parse_pdf(dprf_ctx *c, const char *const *f) {
     return DPRF_OK;
 }
 
+/* candidates per launch, sized for ~0.05-0.2 s of device time per launch at the measured rates */
+static uint32_t chunk_for(kernel_kind k) {
+    switch (k) {
+        case K_OFFICE: return 1u << 19;
+        case K_ODT: return 1u << 22;
+        case K_PDF_R24: return 1u << 24;
+        case K_PDF_R5: return 1u << 27;
+        case K_PDF_R6: return 1u << 18;
+        default: return 1u << 24;
+    }
+}
+
 /* ------------------------------------------------------------------ ABI: library */
 extern "C" int dprf_abi_version(void) { return DPRF_ABI_VERSION; }
 extern "C" const char *dprf_last_error(void) { return g_err.c_str(); }
@@ -325,6 +338,7 @@ extern "C" int dprf_ctx_destroy(dprf_ctx *c) {
     (void)hipFree(c->d_res);
     (void)hipFree(c->d_slots);
     (void)hipFree(c->d_lens);
+    (void)hipFree(c->d_keys);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -359,6 +373,12 @@ extern "C" int dprf_ctx_create(const char *const *fields, int nfields, int devic
         dprf_ctx_destroy(c);
         return fail(DPRF_E_HIP, "context allocation: %s", hipGetErrorString(e));
     }
+    if (c->kind == K_OFFICE || c->kind == K_ODT) {
+        if ((e = hipMalloc(&c->d_keys, (size_t)8 * sizeof(uint32_t) * chunk_for(c->kind))) != hipSuccess) {
+            dprf_ctx_destroy(c);
+            return fail(DPRF_E_HIP, "key hand-off buffer: %s", hipGetErrorString(e));
+        }
+    }
     *out = c;
     return DPRF_OK;
 }
@@ -367,22 +387,10 @@ extern "C" int dprf_ctx_flags(const dprf_ctx *c) { return c ? c->flags : DPRF_E_
 extern "C" const char *dprf_ctx_kernel(const dprf_ctx *c) { return c ? kind_name(c->kind) : "none"; }
 
 /* ------------------------------------------------------------------ launching */
-/* candidates per launch, sized for ~0.05-0.2 s of device time per launch at the measured rates */
-static uint32_t chunk_for(kernel_kind k) {
-    switch (k) {
-        case K_OFFICE: return 1u << 19;
-        case K_ODT: return 1u << 22;
-        case K_PDF_R24: return 1u << 24;
-        case K_PDF_R5: return 1u << 27;
-        case K_PDF_R6: return 1u << 18;
-        default: return 1u << 24;
-    }
-}
-
 static hipError_t launch(dprf_ctx *c, const dprf_enum &e, uint32_t cap, uint32_t stop) {
     switch (c->kind) {
-        case K_OFFICE: return launch_office(e, c->office, c->d_tables, c->d_res, cap, stop, c->stream);
-        case K_ODT: return launch_odt(e, c->odt, c->d_tables, c->d_res, cap, stop, c->stream);
+        case K_OFFICE: return launch_office(e, c->office, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys);
+        case K_ODT: return launch_odt(e, c->odt, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys);
         case K_PDF_R24: return launch_pdf_r24(e, c->pdf, c->d_res, cap, stop, c->stream);
         case K_PDF_R5: return launch_pdf_r5(e, c->pdf, c->d_res, cap, stop, c->stream);
         case K_PDF_R6: return launch_pdf_r6(e, c->pdf, c->d_tables, c->d_res, cap, stop, c->stream);

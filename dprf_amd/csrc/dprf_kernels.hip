@@ -1,8 +1,8 @@
 /* dprf_kernels.hip -- gfx950 verification kernels, one candidate per lane.
  *
  * Each kernel restates one reference verify() for a batch of candidates:
- *   k_office   msoffcrypto_password_verifier.c:56-191  (SHA-1 x50,002 + AES-128-ECB check)
- *   k_odt      odt_password_verifier.c:51-126          (SHA-256, PBKDF2-HMAC-SHA1 x1024, AES-256-CBC)
+ *   k_office_kdf + k_office_check   msoffcrypto_password_verifier.c:56-191  (SHA-1 x50,002; AES-128-ECB check)
+ *   k_odt_kdf + k_odt_check         odt_password_verifier.c:51-126  (SHA-256, PBKDF2-HMAC-SHA1 x1024; AES-256-CBC)
  *   k_pdf_r24  pdf_password_verifier.c:134-191         (MD5 [x50] + RC4 [x20], S-box in LDS)
  *   k_pdf_r5   pdf_password_verifier.c:194-221         (one SHA-256)
  *   k_pdf_r6   pdf_password_verifier.c:226-291         (dprf_kernels_r6.hip)
@@ -140,17 +140,19 @@ DEVI void sha256_msg2(uint32_t m[32], uint32_t total, uint32_t out[8]) {
 }
 
 /* ================================================================== Office (ECMA-376 Standard) */
+/* Two launches per batch.  k_office_kdf runs the 50,002 dependent SHA-1s at 8 waves/SIMD (<= 64 VGPRs)
+ * and leaves the AES-128 key X1[0:16] of every candidate in HBM ([word][candidate], coalesced);
+ * k_office_check does the AES-128 verifier check with its own register budget.  The hand-off costs
+ * 32 bytes per candidate against ~3e7 issue slots of hashing. */
 template <int MODE>
 __global__ void __launch_bounds__(256, 8)
-k_office(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
-         uint32_t stop_on_first) {
+k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
     __shared__ uint8_t cs[256];
-    __shared__ aes_lds L;
     __shared__ uint32_t flag;
-    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = g0 < e.count;
-    const uint32_t g = valid ? g0 : e.count - 1;
+    if (g0 >= e.count) return;
+    const uint32_t g = g0;
     cand c;
     get_candidate<MODE, true>(e, cs, g, c);
 
@@ -186,9 +188,25 @@ k_office(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_resul
         uint32_t w2[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512u};
         sha1_compress(x1, w2);
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) keys[(size_t)k * e.count + g] = x1[k];
+}
+
+__global__ void __launch_bounds__(256)
+k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
+               uint32_t stop_on_first, const uint32_t *keys) {
+    __shared__ uint8_t cs[256];
+    __shared__ aes_lds L;
+    __shared__ uint32_t flag;
+    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g < e.count;
+    uint32_t key[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) key[k] = valid ? keys[(size_t)k * e.count + g] : 0u;
     /* AES-128-ECB decrypt of verifier and verifier hash, always AES-128 (:159-172, :207) */
     uint32_t rk[44], dk[44];
-    aes128_expand(L, x1, rk);
+    aes128_expand(L, key, rk);
     aes_dec_schedule<10>(L, rk, dk);
     uint32_t dv[4], dh0[4], dh1[4];
     aes_decrypt<10>(L, dk, p.ev, dv);
@@ -197,8 +215,9 @@ k_office(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_resul
     /* decryptedVerifierHash[hash_size] == 0 (:168), hash_size uniform in [0,32) */
     const uint32_t hs = p.hash_size;
     const uint32_t wi = (hs & 15u) >> 2, sh = 24u - 8u * (hs & 3u);
-    const uint32_t *blk = hs < 16u ? dh0 : dh1;
-    uint32_t word = wi == 0 ? blk[0] : wi == 1 ? blk[1] : wi == 2 ? blk[2] : blk[3];
+    uint32_t word;
+    if (hs < 16u) word = wi == 0 ? dh0[0] : wi == 1 ? dh0[1] : wi == 2 ? dh0[2] : dh0[3];
+    else word = wi == 0 ? dh1[0] : wi == 1 ? dh1[1] : wi == 2 ? dh1[2] : dh1[3];
     bool ok = ((word >> sh) & 0xffu) == 0u;
     /* SHA1(verifier) == dec_evh[0:20] (:175-188) */
     uint32_t vh[5];
@@ -213,17 +232,17 @@ k_office(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_resul
 }
 
 /* ================================================================== ODF 1.2 (AES-256-CBC, PBKDF2-HMAC-SHA1) */
+/* Two launches per batch, as for Office: k_odt_kdf (SHA-256 start key + PBKDF2, 8 waves/SIMD) leaves the
+ * 32-byte AES-256 key of every candidate in HBM; k_odt_check decrypts and verifies. */
 template <int MODE>
 __global__ void __launch_bounds__(256, 8)
-k_odt(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
-      uint32_t stop_on_first) {
+k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
     __shared__ uint8_t cs[256];
-    __shared__ aes_lds L;
     __shared__ uint32_t flag;
-    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = g0 < e.count;
-    const uint32_t g = valid ? g0 : e.count - 1;
+    if (g0 >= e.count) return;
+    const uint32_t g = g0;
     cand c;
     get_candidate<MODE, false>(e, cs, g, c);
 
@@ -271,6 +290,22 @@ k_odt(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R,
         if (blkno == 1) { key[0] = t[0]; key[1] = t[1]; key[2] = t[2]; key[3] = t[3]; key[4] = t[4]; }
         else { key[5] = t[0]; key[6] = t[1]; key[7] = t[2]; }
     }
+#pragma unroll
+    for (int k = 0; k < 8; k++) keys[(size_t)k * e.count + g] = key[k];
+}
+
+__global__ void __launch_bounds__(256)
+k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
+            uint32_t stop_on_first, const uint32_t *keys) {
+    __shared__ uint8_t cs[256];
+    __shared__ aes_lds L;
+    __shared__ uint32_t flag;
+    if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = g < e.count;
+    uint32_t key[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) key[k] = valid ? keys[(size_t)k * e.count + g] : 0u;
     /* AES-256-CBC decrypt, no padding (:90-92) */
     uint32_t rk[60], dk[60];
     aes256_expand(L, key, rk);
@@ -510,15 +545,17 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
 #define GRID(n, b) dim3(((n) + (b) - 1) / (b))
 
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
-                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_office<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
-    else hipLaunchKernelGGL(k_office<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys) {
+    if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
 hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
-                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_odt<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
-    else hipLaunchKernelGGL(k_odt<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop);
+                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys) {
+    if (e.mode == 0) hipLaunchKernelGGL(k_odt_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_odt_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    hipLaunchKernelGGL(k_odt_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,

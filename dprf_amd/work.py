@@ -1,60 +1,126 @@
 """Algorithmic work per candidate, for the VALU roofline (DESIGN.md section "Roofline").
 
-Two units are kept side by side:
+Peak.  gfx950 issues one wave64 VALU instruction per SIMD every 2 cycles for FULL-RATE integer ops, i.e.
+256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.64e12 lane-slots/s.  Measured on MI355X
+(profiles/valu_issue_rates_r01.txt, tools/valu_peak.hip): v_add/v_sub/v_xor/v_and/v_or/v_not/v_lshrrev_b32
+reach 96-98% of that; v_lshlrev_b32, v_alignbit (rotate), v_alignbyte, v_perm, v_bfe, v_add3, v_and_or,
+v_lshl_or, v_sad_u8, v_mul_u32_u24 issue at half rate (2 slots); v_bitop3 at 0.59 (1.7 slots).
 
-* SURVEY.md 8(d) "spec ops": 2-input 32-bit operation equivalents, a 3-input op counted as 2
-  (SHA1c ~= 1001, SHA256c ~= 2296, ...).  This is the survey's per-unit figure.
-* gfx950 "instruction floor": the fewest VALU lane-instructions the algorithm needs on gfx950, whose
-  3-input instructions (v_bitop3_b32, v_add3_u32, v_alignbit_b32 as a rotate) retire several spec ops
-  at once.  The roofline uses this unit, because the hardware peak (256 CU x 4 SIMD x 32 lanes x
-  2.4 GHz = 78.64e12 lane-instructions/s) is an instruction-issue rate; a kernel executing more
-  instructions than the floor shows up as a lower fraction, never a higher one.
+Floor.  The per-candidate work is the fewest issue slots the ALGORITHM needs on gfx950 with that cost
+table, derived per primitive from its dataflow (sha1_floor() below does it exactly from which message
+words are constant); a kernel that spends more slots than the floor shows a lower fraction of peak.
 
-Per-primitive floors (derivation in DESIGN.md):
-  SHA1c   597  = 80 rounds x 5 (rol5, f, add3, add, rol30) + 64 schedule x 3 (xor3, xor, rol1) + 5
-  SHA256c 1320 = 64 x 13 + 48 x 10 + 8
-  SHA512c 3256 = 80 x 27 + 64 x 17 + 8          (64-bit ops on 32-bit lanes)
-  MD5c    320  = 64 x 5
-  AES-128 encrypt block 416, AES-128 decrypt block 412, AES-256 decrypt block 572 (T-tables in LDS:
-  2 VALU per lookup + 2 xor3 per column, 40 per round)
-  AES-128 key expansion 160; AES-256 expansion + decryption schedule 1300; AES-128 ditto 900
-  RC4 KSA 832 VALU (+1088 LDS ops); RC4 PRGA byte 8 VALU (+5 LDS ops)
+The survey's own per-unit figures (SURVEY.md 8(d), 2-input spec ops, 3-input op = 2) are kept in SPEC for
+reference.
 """
 
-PEAK_LANE_INSTR_PER_S = 256 * 4 * 32 * 2.4e9   # 78.64e12
+PEAK_SLOTS_PER_S = 256 * 4 * 32 * 2.4e9   # 78.64e12 full-rate VALU lane-slots/s
+PEAK_LANE_INSTR_PER_S = PEAK_SLOTS_PER_S   # backwards-compatible name
 
+# measured issue cost in full-rate slots
+COST = {"add": 1.0, "xor": 1.0, "and": 1.0, "or": 1.0, "shr": 1.0, "shl": 2.0, "rot": 2.0, "bitop3": 1.7,
+        "add3": 2.0, "perm": 2.0, "bfe": 2.0}
+
+
+def sha1_floor(const_words, uniform_words=()):
+    """Issue-slot floor of one SHA-1 compression whose message words `const_words` are compile-time
+    constants and `uniform_words` are wave-uniform (scalar unit, free for the VALU).  The chaining value
+    is variable.  Per round: rol5 + f + (terms-1) additions + rol30; per schedule word: the XOR of its
+    non-constant inputs + rol1."""
+    kind = ["v"] * 16
+    for i in const_words:
+        kind[i] = "c"
+    for i in uniform_words:
+        kind[i] = "u"
+    w = list(kind)
+    slots = 0.0
+    for t in range(80):
+        if t >= 16:
+            ins = [w[t - 3], w[t - 8], w[t - 14], w[t - 16]]
+            nv = sum(1 for x in ins if x == "v")
+            if nv == 0:
+                wt = "u" if "u" in ins else "c"
+            else:
+                slots += {1: 0, 2: COST["xor"], 3: COST["bitop3"], 4: COST["bitop3"] + COST["xor"]}[nv] + COST["rot"]
+                wt = "v"
+            w.append(wt)
+        wt = w[t]
+        # a' = rol5(a) + f(b,c,d) + e + (K + W): K+W folds when W is not a VGPR value
+        terms = 3 + (1 if wt == "v" else 0) + (1 if wt != "v" else 0)   # rol5, f, e, W, [K(+W)]
+        terms = 4 if wt != "v" else 5
+        slots += COST["rot"] + COST["bitop3"] + (terms - 1) * COST["add"] + COST["rot"]
+    return slots + 5 * COST["add"]
+
+
+def sha256_floor():
+    rnd = 3 * COST["rot"] + COST["bitop3"] + COST["bitop3"] + 4 * COST["add"] + 3 * COST["rot"] + COST["bitop3"] \
+        + COST["bitop3"] + 2 * COST["add"] + COST["add"]
+    sched = 2 * (2 * COST["rot"] + COST["shr"] + COST["bitop3"]) + 3 * COST["add"]
+    return 64 * rnd + 48 * sched + 8 * COST["add"]
+
+
+def sha512_floor():
+    add64, rot64, shr64, x64 = 2 * COST["add"], 2 * COST["rot"], COST["rot"] + COST["shr"], 2 * COST["bitop3"]
+    rnd = (3 * rot64 + x64) + x64 + 4 * add64 + (3 * rot64 + x64) + x64 + 2 * add64 + add64
+    sched = 2 * (2 * rot64 + shr64 + x64) + 3 * add64
+    return 80 * rnd + 64 * sched + 8 * add64
+
+
+def md5_floor(n_const_words=0):
+    # F/G/H/I as one bitop3, a + f + (K + M) (K+M folds for constant M), rotate, + b
+    var = 64 * (COST["bitop3"] + 3 * COST["add"] + COST["rot"] + COST["add"])
+    return var - n_const_words * 4 * COST["add"]
+
+
+# AES with the four T-tables in LDS: 2 slots per table index (shift/and, or and + 16-bit shift),
+# 2 x bitop3 per output column (4 table words + round key), last round S-box bytes reassembled.
+AES_ROUND = 16 * 2 * COST["add"] + 4 * 2 * COST["bitop3"]
+AES_LAST = 16 * 2 * COST["add"] + 4 * (3 * COST["perm"] + COST["xor"])
 FLOOR = {
-    "sha1c": 597, "sha256c": 1320, "sha512c": 3256, "md5c": 320,
-    "aes128_enc_block": 416, "aes128_dec_block": 412, "aes256_dec_block": 572,
-    "aes128_keyexp": 160, "aes128_dec_sched": 900, "aes256_keyexp_dec_sched": 1300,
-    "rc4_ksa": 832, "rc4_prga_byte": 8,
+    "sha1c": sha1_floor(()),                                   # generic, all 16 words variable
+    "sha1c_office_loop": sha1_floor(range(6, 16), (0,)),       # W0 = bswap(i) uniform, W1..W5 = H
+    "sha1c_hmac20": sha1_floor(range(5, 16)),                  # PBKDF2 iteration: 20-byte message
+    "sha256c": sha256_floor(), "sha512c": sha512_floor(), "md5c": md5_floor(), "md5c_16": md5_floor(12),
+    "aes128_enc_block": 9 * AES_ROUND + AES_LAST + 4 * COST["xor"] + 4 * COST["xor"],   # + CBC xor
+    "aes128_dec_block": 9 * AES_ROUND + AES_LAST + 4 * COST["xor"],
+    "aes256_dec_block": 13 * AES_ROUND + AES_LAST + 8 * COST["xor"],                    # + CBC xor
+    "aes128_keyexp": 10 * (4 * 2 * COST["add"] + 3 * COST["perm"] + 5 * COST["xor"]),
+    "aes128_dec_sched": 9 * 4 * (4 * 2 * COST["add"] + 4 * 2 * COST["add"] + 2 * COST["bitop3"]),
+    "aes256_keyexp_dec_sched": 7 * (8 * 2 * COST["add"] + 6 * COST["perm"] + 9 * COST["xor"])
+    + 13 * 4 * (4 * 2 * COST["add"] + 4 * 2 * COST["add"] + 2 * COST["bitop3"]),
+    # RC4: per KSA step j += S[i] + k (2 adds) and the S[j] address (and, shift, or = 4); the S[i]
+    # address is an immediate.  PRGA byte: j update, two addresses, xor into the output byte.
+    "rc4_ksa": 256 * (2 * COST["add"] + COST["and"] + COST["shl"] + COST["or"]) + 64 * COST["add"],
+    "rc4_prga_byte": 2 * COST["add"] + 2 * (COST["and"] + COST["shl"] + COST["or"]) + COST["shl"] + COST["xor"],
 }
 SPEC = {
-    "sha1c": 1001, "sha256c": 2296, "sha512c": 5840, "md5c": 532,
-    "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
-    "aes128_keyexp": 0, "aes128_dec_sched": 0, "aes256_keyexp_dec_sched": 0,
-    "rc4_ksa": 2304, "rc4_prga_byte": 16,
+    "sha1c": 1001, "sha1c_office_loop": 1001, "sha1c_hmac20": 1001, "sha256c": 2296, "sha512c": 5840,
+    "md5c": 532, "md5c_16": 532, "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
+    "aes128_keyexp": 0, "aes128_dec_sched": 0, "aes256_keyexp_dec_sched": 0, "rc4_ksa": 2304, "rc4_prga_byte": 16,
 }
 
 # Exact primitive counts per candidate (cross-checked against oracle.work_counts in
-# tests/test_work_accounting.py).  R6 depends on the candidate; its figure is the mean over 1,000
-# random 6-letter candidates of the oracle's counts (tests/test_work_accounting.py regenerates it).
+# tests/test_work_accounting.py).
 COUNTS = {
-    # Office, salt 16, L <= 19: H0 1 + 50,000 + final 1 + X1 2; the verifier hash (1 more SHA1c) is
-    # only reached by the 1/256 of candidates whose decrypted hash passes the zero-byte check (:168)
-    "office": {"sha1c": 50004, "aes128_dec_block": 3, "aes128_keyexp": 1, "aes128_dec_sched": 1},
-    # ODF standard stream (enc_len >= 1024): SHA256(pw) 1 + 1 KiB checksum 17; PBKDF2 2 + 2 x (2 + 1023 x 2)
-    "odt": {"sha256c": 18, "sha1c": 4098, "aes256_dec_block": 64, "aes256_keyexp_dec_sched": 1},
-    # ODF -e stream (enc_len 16)
-    "odt_e": {"sha256c": 1, "sha1c": 4098, "aes256_dec_block": 1, "aes256_keyexp_dec_sched": 1},
-    # PDF R3/R4: initial MD5 2 blocks + 50; 20 x (KSA + 16 PRGA bytes).  MD5(PAD || ID) is document-
-    # constant (the reference recomputes it per candidate, :167); not counted.
-    "pdf_r34": {"md5c": 52, "rc4_ksa": 20, "rc4_prga_byte": 320},
+    # Office, salt 16, L <= 19: H0 1 + 50,000 loop + final 1 + X1 2.  The verifier hash (1 more SHA1c)
+    # is only reached by the 1/256 of candidates whose decrypted hash passes the zero-byte check (:168).
+    "office": {"sha1c_office_loop": 50000, "sha1c": 4, "aes128_dec_block": 3, "aes128_keyexp": 1,
+               "aes128_dec_sched": 1},
+    # ODF standard stream (enc_len >= 1024): SHA256(pw) 1 + 1 KiB checksum 17;
+    # PBKDF2: ipad/opad midstates 2 + 2 blocks x (U1: 2 + 1023 x 2)
+    "odt": {"sha256c": 18, "sha1c": 4, "sha1c_hmac20": 4094, "aes256_dec_block": 64, "aes256_keyexp_dec_sched": 1},
+    "odt_e": {"sha256c": 1, "sha1c": 4, "sha1c_hmac20": 4094, "aes256_dec_block": 1, "aes256_keyexp_dec_sched": 1},
+    # PDF R3/R4: initial MD5 2 blocks + 50 (16-byte message); 20 x (KSA + 16 PRGA bytes).
+    # MD5(PAD || ID) is document-constant (the reference recomputes it per candidate, :167); not counted.
+    "pdf_r34": {"md5c": 2, "md5c_16": 50, "rc4_ksa": 20, "rc4_prga_byte": 320},
     "pdf_r2": {"md5c": 2, "rc4_ksa": 1, "rc4_prga_byte": 32},
     "pdf_r5": {"sha256c": 1},
     # PDF R6, L = 6: mean over 1,000 random lowercase candidates (69.9 rounds)
     "pdf_r6": {"sha256c": 1284.13, "sha512c": 1295.0, "aes128_enc_block": 15027.18, "aes128_keyexp": 69.89},
 }
+# which resource bounds each format (RC4 formats are LDS-bound)
+BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "lds", "pdf_r2": "lds", "pdf_r5": "valu",
+         "pdf_r6": "valu"}
 
 
 def per_candidate(fmt, unit="floor"):

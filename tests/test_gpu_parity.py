@@ -33,14 +33,37 @@ def test_kernel_families(dprf, streams):
             assert fam == want[name.split("_")[0]], (name, fam)
 
 
+def device_limit_ok(name, pw, streams):
+    """Candidates the kernels take (DPRF_MAX_PW): Office <= 32 UTF-16 code units, PDF R2-R4 any length
+    (truncated at 32 like the reference), R5 <= 64 bytes after its 127-byte truncation, others <= 64 bytes."""
+    b = pw.encode()
+    s = streams[name]["stream"]
+    if "$office$" in s:
+        return len(pw.encode("utf-16-le")) <= 64
+    if "$pdf$*" in s and s.split("*")[2] in ("2", "3", "4"):
+        return True
+    return len(b) <= 64
+
+
 def test_verdict_tables_match_reference(dprf, streams, verdicts):
     for name, table in verdicts.items():
         c = ctx_for(dprf, streams, name)
+        table = [(p, v) for p, v in table if device_limit_ok(name, p, streams)]
         cands = [p for p, _ in table]
         hits, n, st = c.verify_list(cands)
         want = [i for i, (_, v) in enumerate(table) if v]
         assert hits == want, (name, [cands[i] for i in hits], [cands[i] for i in want])
         assert st["candidates"] == len(cands)
+
+
+def test_over_limit_candidates_raise(dprf, streams, verdicts):
+    for name, table in verdicts.items():
+        over = [p for p, _ in table if not device_limit_ok(name, p, streams)]
+        if not over:
+            continue
+        with pytest.raises(dprf.DprfError) as ei:
+            ctx_for(dprf, streams, name).verify_list(over)
+        assert ei.value.code == dprf.E_PWLEN
 
 
 def test_hitsets_match_reference(dprf, streams, hitsets):

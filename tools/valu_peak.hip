@@ -21,6 +21,41 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
             if (OP == 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
             if (OP == 2) asm volatile("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
             if (OP == 3) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 5) asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 6) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 7) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 8) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 9) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 10) asm volatile("v_lshlrev_b32_e32 %0, 3, %0" : "+v"(x[c]));
+            if (OP == 11) { asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                            asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y)); }
+            if (OP == 12) asm volatile("v_alignbit_b32 %0, %1, %2, 27" : "=v"(x[c]) : "v"(x[c]), "v"(y));
+            if (OP == 13) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(x[c]));
+            if (OP == 14) asm volatile("v_add3_u32 %0, %0, %1, %0" : "+v"(x[c]) : "s"(seed));
+            if (OP == 15) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 16) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 17) asm volatile("v_or_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 18) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 19) asm volatile("v_lshrrev_b32_e32 %0, 3, %0" : "+v"(x[c]));
+            if (OP == 20) asm volatile("v_alignbyte_b32 %0, %0, %1, 1" : "+v"(x[c]) : "v"(y));
+            if (OP == 21) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 22) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 23) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 24) asm volatile("v_not_b32_e32 %0, %0" : "+v"(x[c]));
+            if (OP == 25) asm volatile("v_sad_u8 %0, %0, 0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 26) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 27) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 28) asm volatile("v_add_lshl_u32 %0, %0, %1, 2" : "+v"(x[c]) : "v"(y));
+            if (OP == 29) asm volatile("v_lshlrev_b16_e32 %0, 3, %0" : "+v"(x[c]));
+            if (OP == 30) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 31) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x[c]) : "v"(y));
+            if (OP == 32) { /* independent VOP3 + VOP2 streams interleaved: even chains alignbit, odd chains xor */
+                if (c & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                else asm volatile("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
+            }
+            if (OP == 33) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 34) asm volatile("v_ashrrev_i32_e32 %0, 3, %0" : "+v"(x[c]));
+            if (OP == 35) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(x[c]) : "v"(x[c]));
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -59,12 +94,37 @@ double run(const char *name, int blocks, int per_iter) {
 }
 
 int main() {
-    for (int blocks : {2048, 8192}) {
-        run<0>("v_add3_u32", blocks, 1);
-        run<1>("v_bitop3_b32", blocks, 1);
-        run<2>("v_alignbit_b32", blocks, 1);
-        run<3>("v_xor_b32", blocks, 1);
-        run<4>("v_lshl_add_u64+", blocks, 1);
-    }
+    const int blocks = 32768;
+    run<3>("v_xor_b32", blocks, 1);
+    run<6>("v_add_u32_e32", blocks, 1);
+    run<23>("v_sub_u32", blocks, 1);
+    run<16>("v_and_b32", blocks, 1);
+    run<17>("v_or_b32", blocks, 1);
+    run<24>("v_not_b32", blocks, 1);
+    run<31>("v_cndmask_b32", blocks, 1);
+    run<35>("v_mov_b32_dpp", blocks, 1);
+    run<30>("v_pk_add_u16", blocks, 1);
+    run<10>("v_lshlrev_b32", blocks, 1);
+    run<19>("v_lshrrev_b32", blocks, 1);
+    run<34>("v_ashrrev_i32", blocks, 1);
+    run<29>("v_lshlrev_b16", blocks, 1);
+    run<2>("v_alignbit_b32", blocks, 1);
+    run<20>("v_alignbyte_b32", blocks, 1);
+    run<8>("v_perm_b32", blocks, 1);
+    run<13>("v_bfe_u32", blocks, 1);
+    run<0>("v_add3_u32", blocks, 1);
+    run<22>("v_xad_u32", blocks, 1);
+    run<26>("v_or3_b32", blocks, 1);
+    run<21>("v_and_or_b32", blocks, 1);
+    run<9>("v_lshl_or_b32", blocks, 1);
+    run<27>("v_lshl_add_u32", blocks, 1);
+    run<28>("v_add_lshl_u32", blocks, 1);
+    run<1>("v_bitop3 0x96", blocks, 1);
+    run<18>("v_bitop3 0xca", blocks, 1);
+    run<33>("v_bitop3 0xe8", blocks, 1);
+    run<25>("v_sad_u8", blocks, 1);
+    run<15>("v_mul_u32_u24", blocks, 1);
+    run<32>("alignbit||xor", blocks, 1);
+    run<11>("add3+xor dep", blocks, 2);
     return 0;
 }
