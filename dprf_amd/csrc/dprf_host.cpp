@@ -306,7 +306,7 @@ static uint32_t chunk_for(kernel_kind k) {
         case K_ODT: return 1u << 22;
         case K_PDF_R24: return 1u << 24;
         case K_PDF_R5: return 1u << 27;
-        case K_PDF_R6: return 1u << 18;
+        case K_PDF_R6: return 1u << 21;
         default: return 1u << 24;
     }
 }

@@ -415,24 +415,59 @@ DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
 
-/* KSA with an NK-byte key held LE-packed in k[4]. */
+/* KSA with an NK-byte key held LE-packed in k[4], software-pipelined across steps.
+ *
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Written straight, every step waits on two dependent
+ * LDS round trips.  Here (a) S[i] is prefetched RC4_PF steps ahead, (b) step i issues its reads BEFORE
+ * the two swap writes of step i-1, and the values are repaired in registers from the swaps the reads
+ * could not see:
+ *   S[j_i]  after steps <= i-1 = (j_i == j_{i-1}) ? s_{i-1} : (j_i == i-1) ? sj_{i-1} : read
+ *   S[i+1]  after steps <= i   = read (made at step i+1-PF, sees steps <= i-PF-1), then for steps
+ *                                k = i-PF .. i in order: (j_k == i+1) ? s_k : value
+ * (S[k] = sj_k is written before S[j_k] = s_k, so the latter wins; S[k] for k < i+1 never aliases
+ * S[i+1]).  The j chain then carries no LDS latency.  Checked against the plain KSA on 20,000 keys by a
+ * Python model of exactly this schedule. */
+#define RC4_PF 4
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
 #pragma unroll
     for (int w = 0; w < 64; w++) *(uint32_t *)(S + (w << 8) + lanebase) = 0x03020100u + 0x04040404u * (uint32_t)w;
-    uint32_t j = 0;
+    uint32_t kb[NK];
+#pragma unroll
+    for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
+    uint32_t yv[RC4_PF];                /* prefetched S[m], slot m % PF */
+    uint32_t hj[RC4_PF + 1], hs[RC4_PF + 1]; /* last PF+1 steps' j and s, slot k % (PF+1) */
+    uint32_t j = 0, s_cur = 0;          /* S[0] = 0 before any swap */
+    uint32_t pj = 0, ps = 0, psj = 0;   /* step i-1's swap, written during step i */
 #pragma unroll
     for (int i = 0; i < 256; i++) {
-        const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
-        const uint32_t si = lds_ld8(S, ai);
-        const int kb = i % NK;
-        const uint32_t kv = (k[kb >> 2] >> (8 * (kb & 3))) & 0xffu;
-        j = j + si + kv;
-        const uint32_t aj = rc4_addr(j, lanebase);
-        const uint32_t sj = lds_ld8(S, aj);
-        lds_st8(S, ai, sj);
-        lds_st8(S, aj, si);
+        const uint32_t ji = (j + s_cur + kb[i % NK]) & 0xffu;
+        uint32_t x = lds_ld8(S, rc4_addr(ji, lanebase));
+        if (i + RC4_PF <= 255) {
+            const int m = i + RC4_PF;
+            yv[m % RC4_PF] = lds_ld8(S, ((uint32_t)(m >> 2) << 8) + (uint32_t)(m & 3) + lanebase);
+        }
+        if (i > 0) {
+            lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, psj);
+            lds_st8(S, rc4_addr(pj, lanebase), ps);
+            x = (ji == pj) ? ps : ((ji == (uint32_t)(i - 1)) ? psj : x);
+        }
+        hj[i % (RC4_PF + 1)] = ji;
+        hs[i % (RC4_PF + 1)] = s_cur;
+        uint32_t s_next = 0;
+        if (i < 255) {
+            const int m = i + 1;
+            s_next = m <= RC4_PF ? (uint32_t)m : yv[m % RC4_PF];
+#pragma unroll
+            for (int kk = (m <= RC4_PF ? 0 : i - RC4_PF); kk <= i; kk++)
+                s_next = (hj[kk % (RC4_PF + 1)] == (uint32_t)m) ? hs[kk % (RC4_PF + 1)] : s_next;
+        }
+        pj = ji; ps = s_cur; psj = x;
+        s_cur = s_next;
+        j = ji;
     }
+    lds_st8(S, (63u << 8) + 3u + lanebase, psj);
+    lds_st8(S, rc4_addr(pj, lanebase), ps);
 }
 /* PRGA of NB bytes XORed into d[] (LE-packed). */
 template <int NB>

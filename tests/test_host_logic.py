@@ -61,3 +61,31 @@ def test_fastdiv_magic_exact():
         for n in [0, 1, d - 1, d, d + 1, 2 ** 32 - 1, 2 ** 31, 2 ** 32 - d] + [rng.getrandbits(32) for _ in range(200)]:
             n &= 0xffffffff
             assert _fastdiv(n, d) == n // d, (n, d)
+
+
+REF_FILES = "/root/reference/test/files"
+
+
+@pytest.mark.parametrize("name,rel,kind", [("pdf_testdoc_r2", "pdf/password_1.3_v1_r2.pdf", "pdf"),
+                                           ("pdf_testdoc_r4", "pdf/password_1.7_v4_r4.pdf", "pdf"),
+                                           ("office_testdoc", "ms/password.docx", "office")])
+def test_parsers_reproduce_reference_streams(streams, name, rel, kind):
+    """The Python-3 parsers print the reference parsers' Python-2 output (PDF streams: SURVEY.md Appendix A,
+    including the escaped ')' in the R2 file's U that Python 3 truncates; Office: office2john.py's output)."""
+    import os
+    path = os.path.join(REF_FILES, rel)
+    if not os.path.exists(path):
+        pytest.skip("reference test document not present")
+    from dprf_amd.parsers import office2john, pdf2john
+    mod = pdf2john if kind == "pdf" else office2john
+    assert mod.get_hash(path) == streams[name]["stream"]
+
+
+def test_get_verification_data_uses_engine_parser_modes(streams, capsys):
+    """brute_force.get_verification_data: doc type 2 uses the -e stream (brute_force.py:239)."""
+    import os
+    if not os.path.exists(REF_FILES):
+        pytest.skip("reference test documents not present")
+    assert bf.get_verification_data("2", REF_FILES + "/odt/password.odt") == streams["odt_testdoc_e"]["stream"]
+    assert bf.get_verification_data("3", REF_FILES + "/pdf/password_1.7_v4_r4.pdf") == streams["pdf_testdoc_r4"]["stream"]
+    assert bf.get_verification_data("1", REF_FILES + "/ms/password.docx") == streams["office_testdoc"]["stream"]

@@ -56,6 +56,13 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
             if (OP == 33) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
             if (OP == 34) asm volatile("v_ashrrev_i32_e32 %0, 3, %0" : "+v"(x[c]));
             if (OP == 35) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(x[c]) : "v"(x[c]));
+            if (OP == 36) asm volatile("v_cmp_eq_u32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %2, vcc" : "+v"(x[c]) : "v"(y), "v"(z) : "vcc");
+            if (OP == 37) { unsigned long long msk; asm volatile("v_cmp_eq_u32_e64 %1, %0, %2\n\tv_cndmask_b32_e64 %0, %0, %3, %1" : "+v"(x[c]), "=s"(msk) : "v"(y), "v"(z)); }
+            if (OP == 38) asm volatile("v_cmp_eq_u32_e32 vcc, %0, %1" : : "v"(x[c]), "v"(y) : "vcc");
+            if (OP == 39) { /* branch-free select: mask = ((a^b)-1) >>arith 31 ; x = ((z^x)&mask)^x */
+                unsigned t;
+                asm volatile("v_xor_b32 %1, %0, %2\n\tv_subrev_u32 %1, 1, %1\n\tv_ashrrev_i32 %1, 31, %1\n\tv_xor_b32 %1, %1, %0\n\tv_and_b32 %1, %1, %3\n\tv_xor_b32 %0, %0, %1" : "+v"(x[c]), "=&v"(t) : "v"(y), "v"(z));
+            }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -96,35 +103,10 @@ double run(const char *name, int blocks, int per_iter) {
 int main() {
     const int blocks = 32768;
     run<3>("v_xor_b32", blocks, 1);
-    run<6>("v_add_u32_e32", blocks, 1);
-    run<23>("v_sub_u32", blocks, 1);
-    run<16>("v_and_b32", blocks, 1);
-    run<17>("v_or_b32", blocks, 1);
-    run<24>("v_not_b32", blocks, 1);
-    run<31>("v_cndmask_b32", blocks, 1);
-    run<35>("v_mov_b32_dpp", blocks, 1);
-    run<30>("v_pk_add_u16", blocks, 1);
-    run<10>("v_lshlrev_b32", blocks, 1);
-    run<19>("v_lshrrev_b32", blocks, 1);
-    run<34>("v_ashrrev_i32", blocks, 1);
-    run<29>("v_lshlrev_b16", blocks, 1);
-    run<2>("v_alignbit_b32", blocks, 1);
-    run<20>("v_alignbyte_b32", blocks, 1);
-    run<8>("v_perm_b32", blocks, 1);
-    run<13>("v_bfe_u32", blocks, 1);
-    run<0>("v_add3_u32", blocks, 1);
-    run<22>("v_xad_u32", blocks, 1);
-    run<26>("v_or3_b32", blocks, 1);
-    run<21>("v_and_or_b32", blocks, 1);
-    run<9>("v_lshl_or_b32", blocks, 1);
-    run<27>("v_lshl_add_u32", blocks, 1);
-    run<28>("v_add_lshl_u32", blocks, 1);
-    run<1>("v_bitop3 0x96", blocks, 1);
-    run<18>("v_bitop3 0xca", blocks, 1);
-    run<33>("v_bitop3 0xe8", blocks, 1);
-    run<25>("v_sad_u8", blocks, 1);
-    run<15>("v_mul_u32_u24", blocks, 1);
-    run<32>("alignbit||xor", blocks, 1);
-    run<11>("add3+xor dep", blocks, 2);
+    run<36>("cmp_e32+cndmask(vcc) pair", blocks, 2);
+    run<37>("cmp_e64+cndmask(sgpr) pair", blocks, 2);
+    run<38>("v_cmp_eq_u32_e32 alone", blocks, 1);
+    run<39>("6-op branchless select", blocks, 6);
+    run<31>("v_cndmask_b32 alone", blocks, 1);
     return 0;
 }
