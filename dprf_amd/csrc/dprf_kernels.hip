@@ -415,19 +415,17 @@ DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
 
-/* KSA with an NK-byte key held LE-packed in k[4], software-pipelined across steps.
+/* KSA with an NK-byte key held LE-packed in k[4], software-pipelined by one step.
  *
- * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Written straight, every step waits on two dependent
- * LDS round trips.  Here (a) S[i] is prefetched RC4_PF steps ahead, (b) step i issues its reads BEFORE
- * the two swap writes of step i-1, and the values are repaired in registers from the swaps the reads
- * could not see:
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  A straight implementation waits on two dependent
+ * LDS round trips per step.  Here step i issues its S[j_i] read and the S[i+1] prefetch BEFORE the two
+ * swap writes of step i-1, so the reads return memory as of step i-2 and are repaired in registers:
  *   S[j_i]  after steps <= i-1 = (j_i == j_{i-1}) ? s_{i-1} : (j_i == i-1) ? sj_{i-1} : read
- *   S[i+1]  after steps <= i   = read (made at step i+1-PF, sees steps <= i-PF-1), then for steps
- *                                k = i-PF .. i in order: (j_k == i+1) ? s_k : value
- * (S[k] = sj_k is written before S[j_k] = s_k, so the latter wins; S[k] for k < i+1 never aliases
- * S[i+1]).  The j chain then carries no LDS latency.  Checked against the plain KSA on 20,000 keys by a
- * Python model of exactly this schedule. */
-#define RC4_PF 4
+ *   S[i+1]  after steps <= i   = (j_i == i+1) ? s_i : (j_{i-1} == i+1) ? s_{i-1} : read
+ * (step i-1 writes S[i-1] = sj_{i-1} first, then S[j_{i-1}] = s_{i-1}, so the latter wins on a tie).
+ * Checked against the plain KSA on 20,000 keys by a Python model of this schedule.  Deeper prefetch
+ * (4 steps, ring of repairs) measured slower: the extra compare/select work costs more than the LDS
+ * latency it hides at 2-3 waves/SIMD. */
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
 #pragma unroll
@@ -435,40 +433,38 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
-    uint32_t yv[RC4_PF];                /* prefetched S[m], slot m % PF */
-    uint32_t hj[RC4_PF + 1], hs[RC4_PF + 1]; /* last PF+1 steps' j and s, slot k % (PF+1) */
-    uint32_t j = 0, s_cur = 0;          /* S[0] = 0 before any swap */
-    uint32_t pj = 0, ps = 0, psj = 0;   /* step i-1's swap, written during step i */
+    uint32_t j = 0;                 /* j_{i-1}, masked */
+    uint32_t s_cur = 0;             /* S[i] after steps <= i-1 (S[0] = 0) */
+    uint32_t pj = 0, ps = 0, psj = 0; /* previous step's j, s, sj (writes pending) */
 #pragma unroll
     for (int i = 0; i < 256; i++) {
         const uint32_t ji = (j + s_cur + kb[i % NK]) & 0xffu;
-        uint32_t x = lds_ld8(S, rc4_addr(ji, lanebase));
-        if (i + RC4_PF <= 255) {
-            const int m = i + RC4_PF;
-            yv[m % RC4_PF] = lds_ld8(S, ((uint32_t)(m >> 2) << 8) + (uint32_t)(m & 3) + lanebase);
-        }
+        const uint32_t aj = rc4_addr(ji, lanebase);
+        uint32_t x = lds_ld8(S, aj);
+        uint32_t y = 0;
+        if (i < 255) y = lds_ld8(S, ((uint32_t)((i + 1) >> 2) << 8) + (uint32_t)((i + 1) & 3) + lanebase);
         if (i > 0) {
+            /* pending writes of step i-1 */
             lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, psj);
             lds_st8(S, rc4_addr(pj, lanebase), ps);
             x = (ji == pj) ? ps : ((ji == (uint32_t)(i - 1)) ? psj : x);
         }
-        hj[i % (RC4_PF + 1)] = ji;
-        hs[i % (RC4_PF + 1)] = s_cur;
-        uint32_t s_next = 0;
+        const uint32_t sj = x;
         if (i < 255) {
-            const int m = i + 1;
-            s_next = m <= RC4_PF ? (uint32_t)m : yv[m % RC4_PF];
-#pragma unroll
-            for (int kk = (m <= RC4_PF ? 0 : i - RC4_PF); kk <= i; kk++)
-                s_next = (hj[kk % (RC4_PF + 1)] == (uint32_t)m) ? hs[kk % (RC4_PF + 1)] : s_next;
+            uint32_t nxt = y;
+            if (i > 0) nxt = (pj == (uint32_t)(i + 1)) ? ps : nxt;
+            nxt = (ji == (uint32_t)(i + 1)) ? s_cur : nxt;
+            pj = ji; ps = s_cur; psj = sj;
+            s_cur = nxt;
+        } else {
+            pj = ji; ps = s_cur; psj = sj;
         }
-        pj = ji; ps = s_cur; psj = x;
-        s_cur = s_next;
         j = ji;
     }
     lds_st8(S, (63u << 8) + 3u + lanebase, psj);
     lds_st8(S, rc4_addr(pj, lanebase), ps);
 }
+
 /* PRGA of NB bytes XORed into d[] (LE-packed). */
 template <int NB>
 DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[NB / 4]) {
