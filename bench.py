@@ -44,6 +44,9 @@ WORKLOADS = {
     "pdf_r5": ("pdf_synth_r5_cat", ALNUM, 7, 1 << 31, "pdf_r5", "PDF R5 (synthetic document), -pr 7 alnum"),
     "odt_e": ("odt_testdoc_e", ALNUM, 6, 1 << 24, "odt_e", "ODF -e 2-byte stream (brute_force.py:239 path), -pr 6 alnum"),
 }
+# rocprofv3 name of the dominant kernel per libdprf kernel family (the one "roofline" times)
+DOMINANT = {"office_std": "k_office_kdf", "odf_aes256": "k_odt_kdf", "pdf_r24": "k_pdf_r24", "pdf_r5": "k_pdf_r5",
+            "pdf_r6": "k_pdf_r6"}
 SIDE_FORMATS = ["office", "pdf_r34", "pdf_r6", "pdf_r2", "pdf_r5"]
 
 
@@ -232,9 +235,10 @@ def main():
     total = cands * world
     launches = sum(s["launches"] for s in stats)
     kern_ms = sum(s["kernel_ms"] for s in stats)
-    avg_launch_ms = kern_ms / max(1, launches)
+    main_ms = sum(s["main_kernel_ms"] for s in stats)
+    avg_launch_ms = main_ms / max(1, launches)          # dominant kernel alone (Office/ODF: the KDF kernel)
     per_launch = cands / max(1, launches)
-    floor = work.per_candidate(wkey)
+    floor = work.per_candidate(wkey, part="main")
     achieved = per_launch * floor / (avg_launch_ms / 1e3)
     peak = work.PEAK_LANE_INSTR_PER_S
     traffic = None
@@ -281,8 +285,11 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T VALU lane-instr/s (gfx950 instruction floor of the algorithm)",
                          "frac": achieved / peak, "traffic": traffic,
+                         "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),
                          "kernel_avg_ms": avg_launch_ms, "candidates_per_launch": per_launch,
                          "floor_instr_per_candidate": floor,
+                         "all_kernels_avg_ms": kern_ms / max(1, launches),
+                         "all_kernels_frac": cands * work.per_candidate(wkey) / (kern_ms / 1e3) / peak,
                          "spec_ops_per_candidate": work.per_candidate(wkey, "spec")},
             "cpu_baseline": cpu,
             "per_format": side,

@@ -10,7 +10,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdprf.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
 FLAG_NEVER_MATCHES, FLAG_REF_NONDETERMINISTIC = 1, 2
@@ -28,7 +28,8 @@ class DprfError(RuntimeError):
 
 class Stats(ctypes.Structure):
     _fields_ = [("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
-                ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("main_kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}

@@ -387,10 +387,10 @@ extern "C" int dprf_ctx_flags(const dprf_ctx *c) { return c ? c->flags : DPRF_E_
 extern "C" const char *dprf_ctx_kernel(const dprf_ctx *c) { return c ? kind_name(c->kind) : "none"; }
 
 /* ------------------------------------------------------------------ launching */
-static hipError_t launch(dprf_ctx *c, const dprf_enum &e, uint32_t cap, uint32_t stop) {
+static hipError_t launch(dprf_ctx *c, const dprf_enum &e, uint32_t cap, uint32_t stop, hipEvent_t mid) {
     switch (c->kind) {
-        case K_OFFICE: return launch_office(e, c->office, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys);
-        case K_ODT: return launch_odt(e, c->odt, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys);
+        case K_OFFICE: return launch_office(e, c->office, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys, mid);
+        case K_ODT: return launch_odt(e, c->odt, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys, mid);
         case K_PDF_R24: return launch_pdf_r24(e, c->pdf, c->d_res, cap, stop, c->stream);
         case K_PDF_R5: return launch_pdf_r5(e, c->pdf, c->d_res, cap, stop, c->stream);
         case K_PDF_R6: return launch_pdf_r6(e, c->pdf, c->d_tables, c->d_res, cap, stop, c->stream);
@@ -408,7 +408,8 @@ static void fastdiv_magic(uint32_t d, uint32_t &m, uint32_t &s) {
 }
 
 struct run_state {
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    struct timing { hipEvent_t a, mid, b; };   /* mid: between KDF and check kernel (Office/ODF), else null */
+    std::vector<timing> ev;
     std::chrono::steady_clock::time_point t0;
 };
 
@@ -435,14 +436,15 @@ static int run_chunks(dprf_ctx *c, uint64_t total, int stop_on_first, uint32_t c
         dprf_enum e;
         memset(&e, 0, sizeof e);
         mk(e, off, n);
-        hipEvent_t a, b;
+        hipEvent_t a, b, mid = nullptr;
         HIPCHK(hipEventCreate(&a));
         HIPCHK(hipEventCreate(&b));
+        if (c->kind == K_OFFICE || c->kind == K_ODT) HIPCHK(hipEventCreate(&mid));
         HIPCHK(hipEventRecord(a, c->stream));
-        hipError_t le = launch(c, e, cap, stop_on_first ? 1u : 0u);
+        hipError_t le = launch(c, e, cap, stop_on_first ? 1u : 0u, mid);
         if (le != hipSuccess) return fail(DPRF_E_HIP, "kernel launch (%s): %s", kind_name(c->kind), hipGetErrorString(le));
         HIPCHK(hipEventRecord(b, c->stream));
-        rs.ev.emplace_back(a, b);
+        rs.ev.push_back({a, mid, b});
         off += n;
         if (stop_on_first && off < total) {
             poll.push_back(b);
@@ -476,18 +478,26 @@ static int finish(dprf_ctx *c, run_state &rs, uint64_t *hits, int64_t cap, int64
     if (hits)
         for (int64_t i = 0; i < cap && i < (int64_t)hv.size(); i++) hits[i] = hv[i];
     if (nhits) *nhits = nh;
-    double kms = 0;
+    double kms = 0, mms = 0;
     for (auto &p : rs.ev) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, p.first, p.second);
+        float ms = 0, m = 0;
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
         kms += ms;
-        (void)hipEventDestroy(p.first);
-        (void)hipEventDestroy(p.second);
+        if (p.mid) {
+            (void)hipEventElapsedTime(&m, p.a, p.mid);
+            mms += m;
+            (void)hipEventDestroy(p.mid);
+        } else {
+            mms += ms;
+        }
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
     }
     if (stats) {
         stats->candidates = c->h_hdr->evaluated;
         stats->launches = rs.ev.size();
         stats->kernel_ms = kms;
+        stats->main_kernel_ms = mms;
         stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - rs.t0).count();
         stats->stopped_early = (uint32_t)stopped;
     }

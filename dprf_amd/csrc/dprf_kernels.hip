@@ -576,16 +576,20 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
 #define GRID(n, b) dim3(((n) + (b) - 1) / (b))
 
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
-                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys) {
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
+                         hipEvent_t mid) {
     if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     else hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
 hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
-                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys) {
+                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
+                         hipEvent_t mid) {
     if (e.mode == 0) hipLaunchKernelGGL(k_odt_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     else hipLaunchKernelGGL(k_odt_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_odt_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }

@@ -4,11 +4,14 @@
 #include <hip/hip_runtime.h>
 #include "dprf_params.h"
 
-/* keys: device scratch of >= 8 * e.count words (the derived keys handed from the KDF to the check kernel) */
+/* keys: device scratch of >= 8 * e.count words (the derived keys handed from the KDF to the check kernel);
+ * mid: if non-null, recorded on s between the KDF kernel and the check kernel (dominant-kernel timing) */
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
-                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys);
+                         dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
+                         hipEvent_t mid);
 hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
-                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys);
+                      dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
+                         hipEvent_t mid);
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                          uint32_t stop, hipStream_t s);
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,

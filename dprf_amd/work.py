@@ -118,11 +118,21 @@ COUNTS = {
     # PDF R6, L = 6: mean over 1,000 random lowercase candidates (69.9 rounds)
     "pdf_r6": {"sha256c": 1284.13, "sha512c": 1295.0, "aes128_enc_block": 15027.18, "aes128_keyexp": 69.89},
 }
+# The part of COUNTS done by the dominant kernel when a format runs as two kernels (Office/ODF: KDF kernel,
+# then a short check kernel on the same stream); single-kernel formats are absent (all of COUNTS).
+MAIN = {
+    "office": {"sha1c_office_loop": 50000, "sha1c": 4},
+    "odt": {"sha256c": 1, "sha1c": 4, "sha1c_hmac20": 4094},
+    "odt_e": {"sha256c": 1, "sha1c": 4, "sha1c_hmac20": 4094},
+}
 # which resource bounds each format (RC4 formats are LDS-bound)
 BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "lds", "pdf_r2": "lds", "pdf_r5": "valu",
          "pdf_r6": "valu"}
 
 
-def per_candidate(fmt, unit="floor"):
+def per_candidate(fmt, unit="floor", part="all"):
+    """Issue slots (unit "floor") or survey spec ops (unit "spec") per candidate; part "main" counts only
+    the dominant kernel's share (MAIN)."""
     table = FLOOR if unit == "floor" else SPEC
-    return sum(table[k] * v for k, v in COUNTS[fmt].items())
+    counts = MAIN.get(fmt, COUNTS[fmt]) if part == "main" else COUNTS[fmt]
+    return sum(table[k] * v for k, v in counts.items())

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 1
+#define DPRF_ABI_VERSION 2
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -64,6 +64,8 @@ typedef struct dprf_stats {
     double wall_ms;        /* host wall time of the call, first launch to last result copy      */
     uint32_t stopped_early;/* 1 if stop_on_first ended the search before the whole range        */
     uint32_t reserved;
+    double main_kernel_ms; /* HIP-event time of the dominant kernel alone: the KDF kernel for Office/ODF
+                              (their check kernel follows it on the same stream), else = kernel_ms  (ABI 2) */
 } dprf_stats;
 
 /* ---- library ---- */
