@@ -145,7 +145,19 @@ DEVI constexpr uint64_t k512(int t) {
     0x4cc5d4becb3e42b6ull,0x597f299cfc657e2aull,0x5fcb6fab3ad6faecull,0x6c44198c4a475817ull};
     return K[t];
 }
-DEVI uint64_t ror64(uint64_t x, int s) { return __builtin_rotateright64(x, s); }
+/* 64-bit rotate / shift on the two 32-bit halves with v_alignbit_b32 (2 slots each): the compiler's own
+ * lowering (v_lshrrev_b64 + v_lshl_add_u64) costs ~4.6 + 2.6 slots, measured (profiles/valu_issue_rates). */
+DEVI uint64_t pack64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+DEVI uint64_t ror64(uint64_t x, int s) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (s == 32) return pack64(lo, hi);
+    if (s < 32) return pack64(__builtin_amdgcn_alignbit(lo, hi, s), __builtin_amdgcn_alignbit(hi, lo, s));
+    return pack64(__builtin_amdgcn_alignbit(hi, lo, s - 32), __builtin_amdgcn_alignbit(lo, hi, s - 32));
+}
+DEVI uint64_t shr64(uint64_t x, int s) {   /* 0 < s < 32 */
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    return pack64(hi >> s, __builtin_amdgcn_alignbit(hi, lo, s));
+}
 DEVI uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
     uint32_t lo = xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
     uint32_t hi = xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
@@ -174,15 +186,15 @@ DEVI void sha512_iv(uint64_t st[8], bool is384) {
 }
 DEVI void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int t = 0; t < 80; t++) {
         uint64_t wt;
         if (t < 16) {
             wt = w[t];
         } else {
             uint64_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
-            uint64_t s0 = xor3_64(ror64(x, 1), ror64(x, 8), x >> 7);
-            uint64_t s1 = xor3_64(ror64(y, 19), ror64(y, 61), y >> 6);
+            uint64_t s0 = xor3_64(ror64(x, 1), ror64(x, 8), shr64(x, 7));
+            uint64_t s1 = xor3_64(ror64(y, 19), ror64(y, 61), shr64(y, 6));
             wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             w[t & 15] = wt;
         }

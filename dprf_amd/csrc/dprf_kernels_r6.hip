@@ -27,22 +27,33 @@
 #include "dprf_params.h"
 #include "dprf_launch.h"
 
-#define R6_TE_COPIES 16
-#define R6_PER_LANE 4           /* candidates per lane per launch (persistent refill) */
+/* Te0 replicated 64x: entry x, copy c at byte 256*x + 4*c.  Lane l reads copy l, so the 32 lanes of a
+ * ds_read_b32 group hit 32 different banks whatever the indices (conflict-free), and the address of
+ * byte k of a state word is ONE v_perm: byte 1 <- byte k of the word, byte 0 <- 4*lane, bytes 2-3 <- 0. */
+#define R6_TE_COPIES 64
+#define R6_TE_BYTES (R6_TE_COPIES * 1024)
 
 DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
     uint32_t t = __umulhi(n, m);
     return (t + ((n - t) >> 1)) >> s;
 }
 
+/* static, so its LDS address is a link-time constant (0) and folds into the ds_read: the v_perm result is
+ * the whole address */
+__shared__ __attribute__((aligned(16))) uint32_t r6_te[R6_TE_BYTES / 4];
+
 struct r6_lds {
-    const uint32_t *te;        /* R6_TE_COPIES x 256 words */
-    uint8_t *pat;              /* [pat_words][64 lanes] words for this wave */
-    uint32_t lanebase;         /* lane * 4 */
-    uint32_t tebase;           /* (lane % 16) */
+    uint8_t *pat;              /* [pat_words][64 lanes] words of the wave that owns the slot */
+    uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
+    uint32_t lanec;            /* 4 * (thread lane): this thread's Te0 copy */
 };
 
-DEVI uint32_t te_(const r6_lds &S, uint32_t x) { return S.te[(x << 4) | S.tebase]; }
+/* Te0[byte k of v] */
+template <int K>
+DEVI uint32_t teb(const r6_lds &S, uint32_t v) {
+    const uint32_t a = __builtin_amdgcn_perm(v, S.lanec, 0x0c0c0000u | ((4u + K) << 8));
+    return *(const uint32_t *)((const uint8_t *)r6_te + a);
+}
 DEVI uint32_t pat_addr(uint32_t pos, uint32_t lanebase) { return ((pos >> 2) << 8) | (pos & 3u) | lanebase; }
 
 DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[44]) {
@@ -53,8 +64,8 @@ DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[4
     for (int i = 0; i < 10; i++) {
         const uint32_t t = rk[4 * i + 3];
         /* SubWord(RotWord(t)) with S[x] = byte 2 of Te0[x] */
-        const uint32_t sw = ((te_(S, B2(t)) << 8) & 0xff000000u) | (te_(S, B1(t)) & 0x00ff0000u) |
-                            ((te_(S, B0(t)) >> 8) & 0x0000ff00u) | ((te_(S, B3(t)) >> 16) & 0xffu);
+        const uint32_t sw = ((teb<2>(S, t) << 8) & 0xff000000u) | (teb<1>(S, t) & 0x00ff0000u) |
+                            ((teb<0>(S, t) >> 8) & 0x0000ff00u) | ((teb<3>(S, t) >> 16) & 0xffu);
         rk[4 * i + 4] = rk[4 * i] ^ sw ^ rcon[i];
         rk[4 * i + 5] = rk[4 * i + 1] ^ rk[4 * i + 4];
         rk[4 * i + 6] = rk[4 * i + 2] ^ rk[4 * i + 5];
@@ -67,29 +78,25 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t t0 = xor3(xor3(te_(S, B3(s0)), ror32(te_(S, B2(s1)), 8), ror32(te_(S, B1(s2)), 16)),
-                                 ror32(te_(S, B0(s3)), 24), rk[4 * r]);
-        const uint32_t t1 = xor3(xor3(te_(S, B3(s1)), ror32(te_(S, B2(s2)), 8), ror32(te_(S, B1(s3)), 16)),
-                                 ror32(te_(S, B0(s0)), 24), rk[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(te_(S, B3(s2)), ror32(te_(S, B2(s3)), 8), ror32(te_(S, B1(s0)), 16)),
-                                 ror32(te_(S, B0(s1)), 24), rk[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(te_(S, B3(s3)), ror32(te_(S, B2(s0)), 8), ror32(te_(S, B1(s1)), 16)),
-                                 ror32(te_(S, B0(s2)), 24), rk[4 * r + 3]);
+        const uint32_t t0 = xor3(xor3(teb<3>(S, s0), ror32(teb<2>(S, s1), 8), ror32(teb<1>(S, s2), 16)),
+                                 ror32(teb<0>(S, s3), 24), rk[4 * r]);
+        const uint32_t t1 = xor3(xor3(teb<3>(S, s1), ror32(teb<2>(S, s2), 8), ror32(teb<1>(S, s3), 16)),
+                                 ror32(teb<0>(S, s0), 24), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(teb<3>(S, s2), ror32(teb<2>(S, s3), 8), ror32(teb<1>(S, s0), 16)),
+                                 ror32(teb<0>(S, s1), 24), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(teb<3>(S, s3), ror32(teb<2>(S, s0), 8), ror32(teb<1>(S, s1), 16)),
+                                 ror32(teb<0>(S, s2), 24), rk[4 * r + 3]);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     /* last round: SubBytes + ShiftRows + AddRoundKey, S[x] = byte 2 of Te0[x] */
-#define SB3(x) ((te_(S, (x)) << 8) & 0xff000000u)
-#define SB2(x) (te_(S, (x)) & 0x00ff0000u)
-#define SB1(x) ((te_(S, (x)) >> 8) & 0x0000ff00u)
-#define SB0(x) ((te_(S, (x)) >> 16) & 0x000000ffu)
-    out[0] = (SB3(B3(s0)) | SB2(B2(s1)) | SB1(B1(s2)) | SB0(B0(s3))) ^ rk[40];
-    out[1] = (SB3(B3(s1)) | SB2(B2(s2)) | SB1(B1(s3)) | SB0(B0(s0))) ^ rk[41];
-    out[2] = (SB3(B3(s2)) | SB2(B2(s3)) | SB1(B1(s0)) | SB0(B0(s1))) ^ rk[42];
-    out[3] = (SB3(B3(s3)) | SB2(B2(s0)) | SB1(B1(s1)) | SB0(B0(s2))) ^ rk[43];
-#undef SB3
-#undef SB2
-#undef SB1
-#undef SB0
+    out[0] = (((teb<3>(S, s0) << 8) & 0xff000000u) | (teb<2>(S, s1) & 0x00ff0000u) |
+              ((teb<1>(S, s2) >> 8) & 0x0000ff00u) | ((teb<0>(S, s3) >> 16) & 0xffu)) ^ rk[40];
+    out[1] = (((teb<3>(S, s1) << 8) & 0xff000000u) | (teb<2>(S, s2) & 0x00ff0000u) |
+              ((teb<1>(S, s3) >> 8) & 0x0000ff00u) | ((teb<0>(S, s0) >> 16) & 0xffu)) ^ rk[41];
+    out[2] = (((teb<3>(S, s2) << 8) & 0xff000000u) | (teb<2>(S, s3) & 0x00ff0000u) |
+              ((teb<1>(S, s0) >> 8) & 0x0000ff00u) | ((teb<0>(S, s1) >> 16) & 0xffu)) ^ rk[42];
+    out[3] = (((teb<3>(S, s3) << 8) & 0xff000000u) | (teb<2>(S, s0) & 0x00ff0000u) |
+              ((teb<1>(S, s1) >> 8) & 0x0000ff00u) | ((teb<0>(S, s2) >> 16) & 0xffu)) ^ rk[43];
 }
 
 /* SHA-512 over 32 BE words held as two 16-word halves; state as 16 BE words (hi, lo pairs) */
@@ -173,10 +180,9 @@ DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8
     return len;
 }
 
-/* One round of the hardened hash for this lane: K, bs updated; returns E[last]. */
-DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t K[16]) {
-    const uint32_t Lp = len + bs;
-    /* period = pw || K[0:bs], then its first 16 bytes again (a 16-byte read at o < Lp never wraps) */
+/* Write K[0:bs] (BE words) at byte `len` of the slot's period and repeat the period's first 16 bytes
+ * after it (a 16-byte block read starting at o < Lp then never wraps). */
+DEVI void r6_store_k(const r6_lds &S, uint32_t len, uint32_t bs, const uint32_t K[16]) {
 #pragma unroll
     for (int k = 0; k < 64; k++) {
         if ((uint32_t)k < bs) {
@@ -184,47 +190,71 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t K[1
             S.pat[pat_addr(len + k, S.lanebase)] = (uint8_t)b;
         }
     }
+    const uint32_t Lp = len + bs;
     for (uint32_t k = 0; k < 16; k++) S.pat[pat_addr(Lp + k, S.lanebase)] = S.pat[pat_addr(k, S.lanebase)];
+}
+
+/* Four BE words starting at byte o of the slot's period (one v_perm per word). */
+DEVI void r6_read16(const r6_lds &S, uint32_t o, uint32_t v[4]) {
+    const uint32_t sel = 0x00010203u + (o & 3u) * 0x01010101u;
+    const uint32_t *col = (const uint32_t *)(S.pat + (((o >> 2) << 8) | S.lanebase));
+    uint32_t lw[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) lw[k] = col[k * 64];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = perm(lw[k + 1], lw[k], sel);
+}
+
+/* K[0:32] of the slot (AES key and IV of the next round), read back from its period. */
+DEVI void r6_load_k(const r6_lds &S, uint32_t len, uint32_t K[8]) {
+    r6_read16(S, len, K);
+    r6_read16(S, len + 16u, K + 4);
+}
+
+/* Hash family of the slot's next round: sum(E[0:16]) mod 3 of the first ciphertext block (:264-268). */
+DEVI uint32_t r6_family(const r6_lds &S, uint32_t len) {
+    uint32_t K[8], rk[44], v[4], y[4];
+    r6_load_k(S, len, K);
+    aes128_expand_te(S, K, rk);
+    r6_read16(S, 0u, v);
+    aes128_encrypt_te(S, rk, v[0] ^ K[4], v[1] ^ K[5], v[2] ^ K[6], v[3] ^ K[7], y);
+    uint32_t sum = __builtin_amdgcn_sad_u8(y[0], 0u, 0u);
+    sum = __builtin_amdgcn_sad_u8(y[1], 0u, sum);
+    sum = __builtin_amdgcn_sad_u8(y[2], 0u, sum);
+    sum = __builtin_amdgcn_sad_u8(y[3], 0u, sum);
+    return sum % 3u;
+}
+
+/* One round of the hardened hash for a slot whose family `hsel` is known: returns E[last]; K (16 BE
+ * words, zero past the digest) and bs become the next round's; K[0:bs] is stored back into the period. */
+DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16]) {
+    const uint32_t Lp = len + bs;
+    r6_load_k(S, len, K);
     /* AES-128 key K[0:16], iv K[16:32] (:259-261) */
     uint32_t rk[44];
     aes128_expand_te(S, K, rk);
     uint32_t prev[4] = {K[4], K[5], K[6], K[7]};
     uint32_t hs[16], half[16];
-    uint32_t hsel = 0;          /* 0: SHA-256, 1: SHA-384, 2: SHA-512 */
+    if (hsel == 0) {
+        sha256_iv(hs);
+    } else {
+        uint64_t iv[8];
+        sha512_iv(iv, hsel == 1);
+#pragma unroll
+        for (int k = 0; k < 8; k++) { hs[2 * k] = (uint32_t)(iv[k] >> 32); hs[2 * k + 1] = (uint32_t)iv[k]; }
+    }
     uint32_t o = 0;
-    for (uint32_t u = 0; u < Lp; u++) {         /* 64-byte units; per-lane trip count */
+    for (uint32_t u = 0; u < Lp; u++) {         /* 64-byte units of data = 64 x period */
         uint32_t w[16];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint32_t wi = o >> 2;
-            const uint32_t sel = 0x00010203u + (o & 3u) * 0x01010101u;
-            const uint32_t *col = (const uint32_t *)(S.pat + ((wi << 8) | S.lanebase));
-            uint32_t lw[5];
-#pragma unroll
-            for (int k = 0; k < 5; k++) lw[k] = col[k * 64];
-            uint32_t y[4];
-            aes128_encrypt_te(S, rk, perm(lw[1], lw[0], sel) ^ prev[0], perm(lw[2], lw[1], sel) ^ prev[1],
-                              perm(lw[3], lw[2], sel) ^ prev[2], perm(lw[4], lw[3], sel) ^ prev[3], y);
+            uint32_t v[4], y[4];
+            r6_read16(S, o, v);
+            aes128_encrypt_te(S, rk, v[0] ^ prev[0], v[1] ^ prev[1], v[2] ^ prev[2], v[3] ^ prev[3], y);
 #pragma unroll
             for (int k = 0; k < 4; k++) { prev[k] = y[k]; w[4 * q + k] = y[k]; }
             o += 16u;
             o = o >= Lp ? o - Lp : o;
-            if (q == 0 && u == 0) {
-                /* Step 4: SHA-2 size from sum(E[0:16]) mod 3 (:264-268) */
-                uint32_t sum = __builtin_amdgcn_sad_u8(y[0], 0u, 0u);
-                sum = __builtin_amdgcn_sad_u8(y[1], 0u, sum);
-                sum = __builtin_amdgcn_sad_u8(y[2], 0u, sum);
-                sum = __builtin_amdgcn_sad_u8(y[3], 0u, sum);
-                hsel = sum % 3u;
-                if (hsel == 0) {
-                    sha256_iv(hs);
-                } else {
-                    uint64_t iv[8];
-                    sha512_iv(iv, hsel == 1);
-#pragma unroll
-                    for (int k = 0; k < 8; k++) { hs[2 * k] = (uint32_t)(iv[k] >> 32); hs[2 * k + 1] = (uint32_t)iv[k]; }
-                }
-            }
         }
         if (hsel == 0) {
             sha256_compress(hs, w);
@@ -258,71 +288,129 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t K[1
 #pragma unroll
     for (int k = 0; k < 16; k++) K[k] = hs[k];
     bs = 32u + 16u * hsel;
+    r6_store_k(S, len, bs, K);
     return prev[3] & 0xffu;
 }
 
+/* Slots and classes.  One workgroup per CU holds up to R6_MAX_SLOTS candidates ("slots"); everything a
+ * slot needs between rounds is in LDS: its period (pw || K[0:bs] || wrap) in a column of the pattern area,
+ * and a state word.  Each round, every thread first finds the hash family of its own slot (one AES
+ * block), the slots are counting-sorted by class = (family is SHA-256 ? 0 : 3) + (bs - 32) / 16 (the data
+ * length is 64 x (len + bs)), and thread t then runs the round of the t-th slot in class order.  Waves
+ * thereby see one hash family and one trip count (up to the class boundaries) instead of running SHA-256
+ * and SHA-384/512 predicated and to the longest period in the wave; slots with no candidate left sort
+ * last, so idle waves skip the round whole.  A finished slot takes the next candidate of the launch from
+ * a global cursor, so no workgroup idles while another still has work. */
+#define R6_MAX_SLOTS 768
+#define R6_CLASSES 7                    /* 6 live classes + "no candidate" */
+#define R6_IDLE 0xffffffffu
+
+struct r6_shared {
+    uint32_t hist[8];
+    uint32_t done;                      /* candidates finished by this workgroup */
+    uint32_t flag;
+    uint32_t state[R6_MAX_SLOTS];       /* len | bs << 8 | round << 16 | family << 30 */
+    uint32_t cand[R6_MAX_SLOTS];        /* candidate offset within the launch, R6_IDLE when none */
+    uint16_t order[R6_MAX_SLOTS];       /* slot run by thread t this round */
+};
+
+DEVI r6_lds slot_lds(uint8_t *patbase, uint32_t pat_words, uint32_t slot, uint32_t lane) {
+    r6_lds S;
+    S.pat = patbase + (size_t)(slot >> 6) * pat_words * 256u;
+    S.lanebase = (slot & 63u) << 2;
+    S.lanec = lane << 2;
+    return S;
+}
+
 template <int MODE>
-__global__ void __launch_bounds__(256, 3)     /* <= 168 VGPRs: 3 waves/SIMD; the unit loop stays spill-free */
+DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, dprf_results *R,
+                   uint32_t stop_on_first, r6_shared *sh, const r6_lds &S, uint32_t slot) {
+    uint32_t c = R6_IDLE;
+    if (!(stop_on_first && __hip_atomic_load(&R->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        c = atomicAdd(&R->cursor, 1u);
+        if (c >= e.count) c = R6_IDLE;
+    }
+    sh->cand[slot] = c;
+    if (c != R6_IDLE) {
+        uint32_t K[16];
+        const uint32_t len = r6_begin<MODE>(e, p, cs, e.start + c, S, K);
+        r6_store_k(S, len, 32u, K);
+        sh->state[slot] = len | (32u << 8);
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(R6_MAX_SLOTS, 1)     /* 12 waves/CU: <= 168 VGPRs */
 k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
          uint32_t stop_on_first, uint32_t pat_words) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *te = smem;                                                   /* 16 KiB */
-    uint8_t *cs = (uint8_t *)(smem + R6_TE_COPIES * 256);                  /* 256 B */
-    uint32_t *flag = smem + R6_TE_COPIES * 256 + 64;
-    uint8_t *patbase = (uint8_t *)(smem + R6_TE_COPIES * 256 + 64 + 4);    /* 4 waves x pat_words x 256 B */
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < R6_TE_COPIES * 256; k += blockDim.x) te[k] = T->te0[k / R6_TE_COPIES];
-    for (uint32_t k = tid; k < 64; k += blockDim.x) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
-    if (tid == 0) *flag = stop_on_first ? __hip_atomic_load(&R->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];               /* after r6_te */
+    uint8_t *cs = (uint8_t *)smem;                                              /* 256 B */
+    r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
+    uint8_t *patbase = (uint8_t *)smem + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, nslots = blockDim.x;
+    for (uint32_t k = tid; k < R6_TE_BYTES / 4; k += nslots) r6_te[k] = T->te0[k / R6_TE_COPIES];
+    for (uint32_t k = tid; k < 64; k += nslots) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
+    if (tid < 8) sh->hist[tid] = 0u;
+    if (tid == 0) sh->done = 0u;
     __syncthreads();
-    if (*flag) return;
 
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    r6_lds S;
-    S.te = te;
-    S.pat = patbase + (size_t)wave * pat_words * 256u;
-    S.lanebase = lane << 2;
-    S.tebase = lane & (R6_TE_COPIES - 1);
-
-    /* this wave's contiguous range of candidates (offsets within the launch) */
-    const uint32_t per_wave = 64u * R6_PER_LANE;
-    const uint32_t wbeg = (blockIdx.x * (blockDim.x >> 6) + wave) * per_wave;
-    const uint32_t wend = min(wbeg + per_wave, e.count);
-    uint32_t next = wbeg + 64u;                  /* wave-uniform: next unassigned offset */
-    uint32_t mine = wbeg + lane;
-    bool act = mine < wend;
-    uint32_t K[16], len = 0, bs = 32, i = 0;
-    if (act) len = r6_begin<MODE>(e, p, cs, e.start + mine, S, K);
-    while (__any(act)) {
-        bool fin = false;
-        if (act) {
-            const uint32_t last = r6_round(S, len, bs, K);
-            i++;
-            fin = i >= 64u && i >= last + 32u;          /* loop condition of :247 */
-            if (fin) {
-                bool ok = true;
+    r6_start<MODE>(e, p, cs, R, stop_on_first, sh, slot_lds(patbase, pat_words, tid, lane), tid);
+    for (;;) {
+        __syncthreads();
+        /* phase 1: family of my own slot; rank within its class by an LDS atomic */
+        uint32_t cls = R6_CLASSES - 1, hsel = 0;
+        if (sh->cand[tid] != R6_IDLE) {
+            const uint32_t st = sh->state[tid];
+            hsel = r6_family(slot_lds(patbase, pat_words, tid, lane), st & 0xffu);
+            cls = (hsel ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
+        }
+        const uint32_t rank = atomicAdd(&sh->hist[cls], 1u);
+        __syncthreads();
+        if (sh->hist[R6_CLASSES - 1] == nslots) break;             /* no slot has a candidate: uniform exit */
+        uint32_t pos = rank;
 #pragma unroll
-                for (int k = 0; k < 8; k++) ok = ok && K[k] == p.u[k];
-                if (ok) {
-                    const unsigned long long idx = e.start + mine;
-                    uint32_t slot = atomicAdd(&R->nhits, 1u);
-                    if (slot < cap) R->hits[slot] = idx;
-                    atomicMin(&R->first, idx);
-                    if (stop_on_first) atomicExch(&R->stop, 1u);
-                }
+        for (uint32_t k = 0; k < R6_CLASSES - 1; k++) pos += k < cls ? sh->hist[k] : 0u;
+        sh->order[pos] = (uint16_t)tid;
+        sh->state[tid] |= hsel << 30;          /* round counter (bits 16..29) < 2^14 */
+        __syncthreads();
+        if (tid < 8) sh->hist[tid] = 0u;
+        /* phase 2: the round of slot order[tid] */
+        const uint32_t slot = sh->order[tid];
+        if (sh->cand[slot] == R6_IDLE) continue;
+        const r6_lds S = slot_lds(patbase, pat_words, slot, lane);
+        const uint32_t st = sh->state[slot];
+        const uint32_t len = st & 0xffu, hs = st >> 30;
+        uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
+        uint32_t K[16];
+        const uint32_t last = r6_round(S, len, bs, hs, K);
+        i++;
+        if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 8; k++) ok = ok && K[k] == p.u[k];
+            if (ok) {
+                const unsigned long long idx = e.start + sh->cand[slot];
+                uint32_t h = atomicAdd(&R->nhits, 1u);
+                if (h < cap) R->hits[h] = idx;
+                atomicMin(&R->first, idx);
+                if (stop_on_first) atomicExch(&R->stop, 1u);
             }
+            atomicAdd(&sh->done, 1u);
+            r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
+        } else {
+            sh->state[slot] = len | (bs << 8) | (i << 16);
         }
-        /* refill finished lanes with the wave's next candidates */
-        const unsigned long long m = __ballot(fin);
-        if (fin) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            mine = next + rank;
-            act = mine < wend;
-            if (act) { bs = 32; i = 0; len = r6_begin<MODE>(e, p, cs, e.start + mine, S, K); }
-        }
-        next += (uint32_t)__popcll(m);
     }
-    if (lane == 0 && wbeg < e.count) atomicAdd(&R->evaluated, (unsigned long long)(wend - wbeg));
+    if (tid == 0 && sh->done) atomicAdd(&R->evaluated, (unsigned long long)sh->done);
+}
+
+/* Waves per workgroup: as many of the 12 the VGPR budget allows as fit next to the 64 KiB table. */
+static uint32_t r6_waves(uint32_t pat_words) {
+    const size_t fixed = R6_TE_BYTES + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
+    const size_t per_wave = (size_t)pat_words * 256u;
+    uint32_t nw = (uint32_t)((160u * 1024u - fixed) / per_wave);
+    if (nw > R6_MAX_SLOTS / 64) nw = R6_MAX_SLOTS / 64;
+    return nw >= 4 ? nw & ~3u : nw;
 }
 
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
@@ -330,16 +418,27 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     const uint32_t lmax = e.mode == 0 ? e.pwlen : 4u * DPRF_SLOT_WORDS;
     /* period (lmax + 64) + 16 wrap bytes, + 4 words read past the last block start */
     const uint32_t pat_words = (lmax + 64u + 16u + 3u) / 4u + 1u;
-    const size_t shm = (size_t)R6_TE_COPIES * 1024u + 256u + 16u + 4u * (size_t)pat_words * 256u;
+    const uint32_t nw = r6_waves(pat_words);
+    if (nw == 0) return hipErrorInvalidValue;
+    const size_t shm = 256 + (sizeof(r6_shared) + 15) / 16 * 16 + (size_t)nw * pat_words * 256u;   /* + static r6_te */
     static bool attr_set[2] = {false, false};
-    const uint32_t per_block = 4u * 64u * R6_PER_LANE;
-    dim3 grid((e.count + per_block - 1) / per_block);
+    /* the work cursor restarts at 0 for every launch (stream-ordered before the kernel) */
+    hipError_t me = hipMemsetAsync(&R->cursor, 0, sizeof(uint32_t), s);
+    if (me != hipSuccess) return me;
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+    /* one workgroup per CU; a launch smaller than the slots it would open uses fewer workgroups */
+    const uint32_t slots = nw * 64u;
+    uint32_t grid = (e.count + slots - 1) / slots;
+    if (grid > (uint32_t)ncu) grid = (uint32_t)ncu;
     if (e.mode == 0) {
-        if (!attr_set[0]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); attr_set[0] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<0>, grid, dim3(256), shm, s, e, p, T, R, cap, stop, pat_words);
+        if (!attr_set[0]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[0] = true; }
+        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(slots), shm, s, e, p, T, R, cap, stop, pat_words);
     } else {
-        if (!attr_set[1]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); attr_set[1] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<1>, grid, dim3(256), shm, s, e, p, T, R, cap, stop, pat_words);
+        if (!attr_set[1]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[1] = true; }
+        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(slots), shm, s, e, p, T, R, cap, stop, pat_words);
     }
     return hipGetLastError();
 }

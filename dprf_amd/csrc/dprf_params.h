@@ -30,6 +30,8 @@ struct dprf_enum {
 struct dprf_results {
     uint32_t nhits;                 /* total hits (may exceed cap) */
     uint32_t stop;                  /* set by a hit when stop_on_first */
+    uint32_t cursor;                /* work cursor of persistent kernels (PDF R6), reset per launch */
+    uint32_t pad_;
     unsigned long long first;       /* lowest hit index (atomicMin), ~0 if none */
     unsigned long long evaluated;   /* candidates evaluated (per-block atomicAdd) */
     unsigned long long hits[1];     /* [cap] */

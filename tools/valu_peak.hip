@@ -63,6 +63,21 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
                 unsigned t;
                 asm volatile("v_xor_b32 %1, %0, %2\n\tv_subrev_u32 %1, 1, %1\n\tv_ashrrev_i32 %1, 31, %1\n\tv_xor_b32 %1, %1, %0\n\tv_and_b32 %1, %1, %3\n\tv_xor_b32 %0, %0, %1" : "+v"(x[c]), "=&v"(t) : "v"(y), "v"(z));
             }
+            if (OP == 40) { /* 64-bit add as a carry pair through VCC */
+                asm volatile("v_add_co_u32_e32 %0, vcc, %0, %2\n\tv_addc_co_u32_e32 %1, vcc, %1, %3, vcc"
+                             : "+v"(x[c]), "+v"(x[(c + 1) & (CHAINS - 1)]) : "v"(y), "v"(z) : "vcc");
+            }
+            if (OP == 41) { unsigned long long v = ((unsigned long long)x[c] << 32) | x[c];
+                asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | y));
+                x[c] = (unsigned)v; }
+            if (OP == 42) { unsigned long long v = ((unsigned long long)x[c] << 32) | y;
+                asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(v)); x[c] = (unsigned)v; }
+            if (OP == 43) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(x[c]) : "v"(x[(c + 3) & (CHAINS - 1)]));
+            if (OP == 44) { /* 64-bit add as VOP3 carry pair with SGPR carry */
+                unsigned long long cc;
+                asm volatile("v_add_co_u32_e64 %0, %2, %0, %3\n\tv_addc_co_u32_e64 %1, %2, %1, %4, %2"
+                             : "+v"(x[c]), "+v"(x[(c + 1) & (CHAINS - 1)]), "=&s"(cc) : "v"(y), "v"(z));
+            }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -103,10 +118,10 @@ double run(const char *name, int blocks, int per_iter) {
 int main() {
     const int blocks = 32768;
     run<3>("v_xor_b32", blocks, 1);
-    run<36>("cmp_e32+cndmask(vcc) pair", blocks, 2);
-    run<37>("cmp_e64+cndmask(sgpr) pair", blocks, 2);
-    run<38>("v_cmp_eq_u32_e32 alone", blocks, 1);
-    run<39>("6-op branchless select", blocks, 6);
-    run<31>("v_cndmask_b32 alone", blocks, 1);
+    run<40>("add_co+addc (vcc) pair", blocks, 2);
+    run<44>("add_co+addc e64 pair", blocks, 2);
+    run<41>("v_lshl_add_u64", blocks, 1);
+    run<42>("v_lshrrev_b64", blocks, 1);
+    run<43>("v_mov_b32", blocks, 1);
     return 0;
 }
