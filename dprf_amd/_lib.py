@@ -8,7 +8,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdprf.so")
+LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
 ABI_VERSION = 2
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3

@@ -407,35 +407,102 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
 /* ================================================================== PDF R2..R4 (MD5 + RC4) */
 /* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
  * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave
- * therefore never conflict, whatever i/j each lane holds. */
+ * therefore never conflict, whatever i/j each lane holds.  The kernel's whole LDS footprint is exactly
+ * these 16 KiB (charset, PAD and the stop flag are overlaid on the S-box area before the first KSA), so
+ * 10 one-wave workgroups fit a CU's 160 KiB. */
 #define RC4_WAVE_BYTES 16384
 DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
     return ((__builtin_amdgcn_ubfe(j, 2, 6)) << 8) | (j & 3u) | lanebase;
 }
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
+DEVI uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-/* KSA with an NK-byte key held LE-packed in k[4], software-pipelined by one step.
+/* KSA with an NK-byte key held LE-packed in k[4], four steps per group.
  *
- * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  A straight implementation waits on two dependent
- * LDS round trips per step.  Here step i issues its S[j_i] read and the S[i+1] prefetch BEFORE the two
- * swap writes of step i-1, so the reads return memory as of step i-2 and are repaired in registers:
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions 4q..4q+3 are one LDS dword of this lane,
+ * so group q reads that dword once and keeps the group's S[i] side of the swaps in a register:
+ *  (A) the j chain runs from registers only: s_r (= S[4q+r] before step r) is byte r of the dword unless
+ *      an earlier step of the group swapped into it (then it is that step's s);
+ *  (B) each step reads S[j_r] and writes S[j_r] = s_r in program order, so every position outside the
+ *      group is current in LDS (one wave's LDS operations complete in order);
+ *  (C) the group's dword is rebuilt with two byte perms per step -- byte r <- S[j_r] (taken from the
+ *      dword itself when j_r falls inside the group, whose LDS copy is stale), byte j_r&3 <- s_r when
+ *      j_r is inside the group -- and stored once.
+ * Per step that is one byte read + one byte write instead of two of each, and one dependent LDS round
+ * trip per four steps.  Measured against the one-step-ahead schedule and a plain KSA on 4 Mi lanes
+ * (tools/rc4_bench.hip, identical output): 390 / 370 / 334 M cand/s for 20 x (KSA + PRGA16); inside
+ * k_pdf_r24 (with MD5 x52 and enumeration) +1 % over one-step-ahead.  At 16 KiB per wave only 9 waves
+ * fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10), and with LDS-array ~45 % and VALU ~60 % busy the
+ * loop is bound by the LDS round trips of 9 waves, not by either pipe. */
+template <int NK>
+DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
+    /* identity: the values are produced by an add chain kept opaque to the compiler, which would otherwise
+     * hoist 63 literal VGPRs out of the pass loop and halve occupancy */
+    uint32_t iv = 0x03020100u;
+#pragma unroll
+    for (int w = 1; w < 64; w++) {
+        iv += 0x04040404u;
+        asm volatile("" : "+v"(iv));
+        *(uint32_t *)(S + (w << 8) + lanebase) = iv;
+    }
+    uint32_t kb[NK];
+#pragma unroll
+    for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
+    uint32_t j = 0;
+    uint32_t W = 0x03020100u;                   /* dword 0 is the identity: no store, no read */
+#pragma unroll
+    for (int q = 0; q < 64; q++) {
+        const uint32_t base = 4u * (uint32_t)q;
+        uint32_t s[4], m[4], x[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+#pragma unroll
+            for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+            s[r] = v;
+            j = j + v + kb[(4 * q + r) % NK];
+            m[r] = j & 0xffu;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t a = rc4_addr(m[r], lanebase);
+            x[r] = lds_ld8(S, a);
+            lds_st8(S, a, s[r]);
+        }
+        uint32_t Wn = 0;
+        if (q < 63) Wn = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        uint32_t Wf = W;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t v = umin32(m[r] - base, 4u);                 /* byte in the group; 4 = outside */
+            const uint32_t idr = 0x03020100u & ~(0xffu << (8 * r));
+            Wf = __builtin_amdgcn_perm(x[r], Wf, idr | (v << (8 * r)));    /* byte r <- S[j_r] */
+            const uint32_t sh = (v << 3) & 31u;                             /* v = 4: no-op selector */
+            Wf = __builtin_amdgcn_perm(s[r], Wf, 0x03020100u + ((4u - v) << sh)); /* byte v <- s_r */
+        }
+        *(uint32_t *)(S + (q << 8) + lanebase) = Wf;
+        W = Wn;
+    }
+}
+
+/* One-step-ahead KSA schedule, used for R2 (one KSA per candidate).  Step i issues its S[j_i] read and
+ * the S[i+1] prefetch BEFORE the two swap writes of step i-1, so the reads return memory as of step i-2
+ * and are repaired in registers:
  *   S[j_i]  after steps <= i-1 = (j_i == j_{i-1}) ? s_{i-1} : (j_i == i-1) ? sj_{i-1} : read
  *   S[i+1]  after steps <= i   = (j_i == i+1) ? s_i : (j_{i-1} == i+1) ? s_{i-1} : read
  * (step i-1 writes S[i-1] = sj_{i-1} first, then S[j_{i-1}] = s_{i-1}, so the latter wins on a tie).
- * Checked against the plain KSA on 20,000 keys by a Python model of this schedule.  Deeper prefetch
- * (4 steps, ring of repairs) measured slower: the extra compare/select work costs more than the LDS
- * latency it hides at 2-3 waves/SIMD. */
+ * A/B on one box (tools/ab_r24.sh, bench.py pdf_r2): 4.98 G cand/s with this schedule and a full 32-byte
+ * PRGA, 4.50 G with the grouped KSA below, 4.77 G with this one plus the 2-byte early reject -- for one
+ * KSA per candidate the extra code and the reject branch cost more than they save. */
 template <int NK>
-DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
+DEVI void rc4_ksa_ahead(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
 #pragma unroll
     for (int w = 0; w < 64; w++) *(uint32_t *)(S + (w << 8) + lanebase) = 0x03020100u + 0x04040404u * (uint32_t)w;
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
-    uint32_t j = 0;                 /* j_{i-1}, masked */
-    uint32_t s_cur = 0;             /* S[i] after steps <= i-1 (S[0] = 0) */
-    uint32_t pj = 0, ps = 0, psj = 0; /* previous step's j, s, sj (writes pending) */
+    uint32_t j = 0, s_cur = 0, pj = 0, ps = 0, psj = 0;
 #pragma unroll
     for (int i = 0; i < 256; i++) {
         const uint32_t ji = (j + s_cur + kb[i % NK]) & 0xffu;
@@ -444,7 +511,6 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
         uint32_t y = 0;
         if (i < 255) y = lds_ld8(S, ((uint32_t)((i + 1) >> 2) << 8) + (uint32_t)((i + 1) & 3) + lanebase);
         if (i > 0) {
-            /* pending writes of step i-1 */
             lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, psj);
             lds_st8(S, rc4_addr(pj, lanebase), ps);
             x = (ji == pj) ? ps : ((ji == (uint32_t)(i - 1)) ? psj : x);
@@ -454,8 +520,7 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             uint32_t nxt = y;
             if (i > 0) nxt = (pj == (uint32_t)(i + 1)) ? ps : nxt;
             nxt = (ji == (uint32_t)(i + 1)) ? s_cur : nxt;
-            pj = ji; ps = s_cur; psj = sj;
-            s_cur = nxt;
+            pj = ji; ps = s_cur; psj = sj; s_cur = nxt;
         } else {
             pj = ji; ps = s_cur; psj = sj;
         }
@@ -464,10 +529,9 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     lds_st8(S, (63u << 8) + 3u + lanebase, psj);
     lds_st8(S, rc4_addr(pj, lanebase), ps);
 }
-
 /* PRGA of NB bytes XORed into d[] (LE-packed). */
 template <int NB>
-DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[NB / 4]) {
+DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
     uint32_t j = 0;
 #pragma unroll
     for (int i = 1; i <= NB; i++) {
@@ -483,15 +547,42 @@ DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[NB / 4]) {
     }
 }
 
+/* Two-byte PRGA for the early reject: the second byte's swap is applied in registers (its stores would
+ * never be read again before the next KSA re-initialises the box). */
+template <>
+DEVI void rc4_prga<2>(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
+    uint32_t j = 0;
+    /* byte 1 */
+    const uint32_t a1 = (0u << 8) + 1u + lanebase;
+    const uint32_t s1 = lds_ld8(S, a1);
+    j = s1 & 0xffu;
+    const uint32_t aj1 = rc4_addr(j, lanebase);
+    const uint32_t sj1 = lds_ld8(S, aj1);
+    lds_st8(S, a1, sj1);
+    lds_st8(S, aj1, s1);
+    const uint32_t k1 = lds_ld8(S, rc4_addr(s1 + sj1, lanebase));
+    /* byte 2: reads after byte 1's swap (in order); its own swap is applied in registers */
+    const uint32_t a2 = 2u + lanebase;
+    const uint32_t s2 = lds_ld8(S, a2);
+    const uint32_t j2 = (j + s2) & 0xffu;
+    const uint32_t sj2 = lds_ld8(S, rc4_addr(j2, lanebase));
+    const uint32_t t = (s2 + sj2) & 0xffu;
+    uint32_t k2 = lds_ld8(S, rc4_addr(t, lanebase));
+    k2 = (t == j2) ? s2 : ((t == 2u) ? sj2 : k2);
+    d[0] ^= k1 | (k2 << 8);
+}
+
 template <int MODE, int R, int NK>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, 3)   /* <= 170 VGPRs: 3 waves/SIMD >= the 2.5 the LDS allows */
 k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
-    __shared__ uint8_t cs[256];
-    __shared__ uint32_t flag;
-    __shared__ uint32_t padw[16];                 /* PAD || PAD bytes for the runtime-offset padding */
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
+    /* overlaid on the S-box area; all reads of these happen before the first KSA writes it (one wave per
+     * workgroup, LDS operations of a wave complete in order) */
+    uint8_t *cs = S;                                      /* charset, 256 B */
+    uint32_t *flag = (uint32_t *)(S + 256);
+    uint32_t *padw = (uint32_t *)(S + 320);               /* PAD || PAD for the runtime-offset padding */
     if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
-    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, &flag)) return;
+    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag)) return;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = g0 < e.count;
     const uint32_t g = valid ? g0 : e.count - 1;
@@ -545,28 +636,40 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             md5_compress(h, m);
         }
     }
+    /* R3/R4 early reject: every pass first produces only 2 keystream bytes and the candidate survives iff
+     * c19[0:2] equals U[0:2] (byte b of each pass is data[b] ^ keystream[b]).  A wave in which some lane
+     * survives (2^-16 per lane) redoes its candidates with the full keystream and the reference's complete
+     * 16-byte compare (:184-189). */
     uint8_t *Sw = S;   /* one wave per block: the whole array is this wave's */
-    bool ok;
+    bool ok = false;
     if (R == 2) {
         /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189) */
         uint32_t d[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-        rc4_ksa<5>(Sw, lanebase, h);
+        rc4_ksa_ahead<5>(Sw, lanebase, h);
         rc4_prga<32>(Sw, lanebase, d);
         ok = true;
 #pragma unroll
         for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
     } else {
         /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
-        uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
-        for (uint32_t x = 0; x < 20u; x++) {
-            const uint32_t xx = x * 0x01010101u;
-            uint32_t k[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-            rc4_ksa<NK>(Sw, lanebase, k);
-            rc4_prga<16>(Sw, lanebase, d);
+        for (uint32_t full = 0; full < 2u; full++) {
+            uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
+            for (uint32_t x = 0; x < 20u; x++) {
+                const uint32_t xx = x * 0x01010101u;
+                uint32_t k[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
+                rc4_ksa<NK>(Sw, lanebase, k);
+                if (full) rc4_prga<16>(Sw, lanebase, d);
+                else rc4_prga<2>(Sw, lanebase, d);
+            }
+            if (full) {
+                ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
+            } else {
+                const bool pre = ((d[0] ^ p.u[0]) & 0xffffu) == 0u;
+                if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
+            }
         }
-        ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
     }
     if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
     count_block(e, R_);
