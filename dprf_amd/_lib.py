@@ -140,6 +140,21 @@ class Context:
                                        1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
         return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()
 
+    def verify_blob(self, blob, offsets, stop_on_first=False, cap=1 << 16):
+        """verify_list without per-candidate Python work: candidate k is blob[offsets[k]:offsets[k+1]]
+        (offsets: n+1 ascending uint64, e.g. a numpy array).  Used by the GPU client for server payloads."""
+        import numpy as np
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offs) - 1
+        if n < 0:
+            raise ValueError("offsets needs n+1 entries")
+        hits = (ctypes.c_uint64 * max(1, cap))()
+        nh = ctypes.c_int64()
+        st = Stats()
+        _check(lib().dprf_verify_list(self._h, bytes(blob), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                      n, 1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
+        return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()
+
     def verify_list(self, passwords, stop_on_first=False, cap=1 << 16):
         """Verify an explicit candidate list (a client payload).  Returns (sorted hit list indices,
         total hits, stats dict)."""

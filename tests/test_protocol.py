@@ -1,0 +1,197 @@
+"""Work-distribution protocol counterparts (dprf_amd.server / dprf_amd.client / dprf_amd.payload) against
+the reference's server.py / client.py behaviour: candidate order (server.py:189-199), payload JSON
+(:285-292), client loop and found report (client.py:36-69), heartbeat (:209-238), re-queue of an inactive
+client's payload (:241-256).  CPU tests drive the real server and client loop over localhost with a
+verifier stub backed by the oracle (the checker); the GPU test runs the real GPU client."""
+import itertools
+import json
+import random
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from dprf_amd import client as cl
+from dprf_amd import payload as pl
+from dprf_amd import server as sv
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _reference_order(cs, n):
+    out = []
+    for x in range(1, n + 1):
+        out.extend("".join(t) for t in itertools.product(cs, repeat=x))
+    return out
+
+
+@pytest.mark.parametrize("cs,n", [("abc", 4), (pl.LOWERCASE, 2), ("xy", 6)])
+def test_keyspace_is_server_order(cs, n):
+    ref = _reference_order(cs, n)
+    ks = pl.Keyspace(cs, n)
+    assert ks.total == len(ref)
+    got = []
+    rng = random.Random(3)
+    g = 0
+    while g < ks.total:
+        step = rng.randint(1, 40)
+        for L, s, c in ks.segments(g, step):
+            got.extend(ks.password(L, s + k) for k in range(c))
+        g += step
+    assert got == ref
+    for i in rng.sample(range(len(ref)), 20):
+        assert ks.global_index(ref[i]) == i
+
+
+def test_keyspace_facts():
+    ks = pl.Keyspace(pl.LOWERCASE, 8)
+    assert ks.total == 217180147158
+    assert ks.global_index("password") == 129052722139
+    assert pl.Keyspace("ab", 3, limit=5).total == 5
+
+
+@pytest.mark.parametrize("cs,n,g0,cnt", [("abc", 3, 0, 39), (pl.LOWERCASE, 3, 700, 100), ("01", 5, 3, 50)])
+def test_build_message_is_json_of_the_payload(cs, n, g0, cnt):
+    ks = pl.Keyspace(cs, n)
+    segs = ks.segments(g0, cnt)
+    raw = pl.build_message("x.pdf:$pdf$*1*2", cs, segs)
+    d = json.loads(raw)
+    assert d["data"] == "x.pdf:$pdf$*1*2"
+    assert d["passwords"] == _reference_order(cs, n)[g0:g0 + cnt]
+
+
+def _roundtrip(msg_obj, raw=None):
+    raw = raw if raw is not None else json.dumps(msg_obj).encode()
+    stream, blob, offs = pl.parse_message(raw)
+    assert stream == msg_obj["data"]
+    assert [pl.candidate(blob, offs, k) for k in range(len(offs) - 1)] == msg_obj["passwords"]
+    assert offs.dtype == np.uint64 and len(offs) == len(msg_obj["passwords"]) + 1
+
+
+def test_parse_message_fast_and_fallback_paths():
+    rng = random.Random(11)
+    alpha = "abcXYZ019 :,[]{}-_"
+    pw = ["".join(rng.choice(alpha) for _ in range(rng.randint(0, 12))) for _ in range(500)]
+    _roundtrip({"data": "doc.docx:$office$*2007*20", "passwords": pw})
+    # the reference (py2 dict order) may put "passwords" first
+    obj = {"passwords": pw[:50], "data": "doc.pdf:$pdf$*4*4"}
+    _roundtrip({"data": obj["data"], "passwords": obj["passwords"]}, json.dumps(obj).encode())
+    # escapes -> json.loads path (quotes, backslashes, non-ASCII as \\u escapes)
+    _roundtrip({"data": 'we"ird\\name.pdf:$pdf$', "passwords": ['a"b', "c\\d", "päss", "€"]})
+    _roundtrip({"data": "d:$odt$", "passwords": []})
+    _roundtrip({"data": "d:$odt$", "passwords": ["", "", "a"]})
+
+
+class _OracleVerifier:
+    """verify(stream, blob, offsets) -> (found, password) on the CPU oracle (test infrastructure)."""
+
+    def __init__(self, oracle):
+        self.oracle = oracle
+        self.ctx = None
+        self.seen = []
+
+    def __call__(self, stream, blob, offsets):
+        if self.ctx is None:
+            self.ctx = self.oracle.Ctx(stream)
+        pws = [pl.candidate(blob, offsets, k) for k in range(len(offsets) - 1)]
+        self.seen.extend(pws)
+        for p in pws:
+            if self.ctx.verify(p.encode()):
+                return 1, p
+        return 0, None
+
+
+def _run_server(srv):
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("pw", srv.run("127.0.0.1", 0)), daemon=True)
+    th.start()
+    assert srv.bound.wait(10)
+    return th, out
+
+
+def test_server_client_end_to_end_finds_password(streams, oracle):
+    d = streams["pdf_synth_r5_cat"]
+    srv = sv.Server(d["stream"], password_range=3, payload_size=997, heartbeat_port=_free_port(), quiet=True)
+    th, out = _run_server(srv)
+    ver = _OracleVerifier(oracle)
+    rc, pw = cl.connect_to_server("127.0.0.1", srv.address[1], "client-1", ver, quiet=True)
+    th.join(10)
+    assert (rc, pw) == (0, "cat")
+    assert out["pw"] == "cat" and srv.found
+    # the client saw exactly the server's order up to the payload that held the password
+    ref = _reference_order(pl.LOWERCASE, 3)
+    assert ver.seen == ref[:len(ver.seen)] and "cat" in ver.seen
+
+
+def test_server_exhausts_keyspace_and_two_clients_split_it(streams, oracle):
+    d = streams["pdf_synth_r5_cat"]
+    srv = sv.Server(d["stream"], password_range=2, payload_size=50, heartbeat_port=_free_port(), quiet=True)
+    th, out = _run_server(srv)
+    vers = [_OracleVerifier(oracle), _OracleVerifier(oracle)]
+    res = [None, None]
+    ths = [threading.Thread(target=lambda k=k: res.__setitem__(
+        k, cl.connect_to_server("127.0.0.1", srv.address[1], "c%d" % k, vers[k], quiet=True))) for k in range(2)]
+    [t.start() for t in ths]
+    [t.join(30) for t in ths]
+    th.join(10)
+    assert out["pw"] is None and not srv.found
+    assert [r[0] for r in res] == [1, 1]          # "No data received from server. Exiting." (client.py:48-50)
+    seen = sorted(vers[0].seen + vers[1].seen, key=lambda p: (len(p), p))
+    assert seen == _reference_order(pl.LOWERCASE, 2)
+    assert srv.counter == 26 + 26 * 26
+
+
+def test_heartbeat_and_inactive_requeue(streams):
+    d = streams["pdf_synth_r5_cat"]
+    hb = _free_port()
+    srv = sv.Server(d["stream"], password_range=2, payload_size=10, heartbeat_port=hb, quiet=True,
+                    inactive_after=0.5, cleanup_every=0.3)
+    th, out = _run_server(srv)
+    # a client takes one payload and disappears
+    c = socket.create_connection(srv.address)
+    c.sendall(cl.prepare_message("ghost", False, None))
+    c.shutdown(socket.SHUT_WR)
+    first = json.loads(cl.recvall(c))
+    c.close()
+    assert first["passwords"] == _reference_order(pl.LOWERCASE, 2)[:10]
+    # heartbeat answers {"found": false}
+    time.sleep(0.2)
+    h = socket.create_connection(("127.0.0.1", hb))
+    h.sendall(cl.prepare_message("ghost", None, None, True))
+    h.shutdown(socket.SHUT_WR)
+    assert json.loads(cl.recvall(h)) == {"found": False}
+    h.close()
+    time.sleep(1.5)                                   # ghost is dropped, its payload re-queued
+    assert all(x.id != "ghost" for x in srv.clients)
+    seen = []
+
+    def ver(stream, blob, offs):
+        seen.extend(pl.candidate(blob, offs, k) for k in range(len(offs) - 1))
+        return 0, None
+    rc, _ = cl.connect_to_server("127.0.0.1", srv.address[1], "late", ver, quiet=True)
+    th.join(10)
+    assert rc == 1
+    assert sorted(seen) == sorted(_reference_order(pl.LOWERCASE, 2))
+
+
+@pytest.mark.gpu
+def test_gpu_client_against_server(streams):
+    """The GPU client (libdprf list mode) finds the password the server's payloads hold."""
+    for name, pr, ps in (("pdf_synth_r4_meta0_dog", 3, 4096), ("office_synth_ok", 2, 300), ("odt_synth_std_zq", 2, 256)):
+        d = streams[name]
+        srv = sv.Server(d["stream"], password_range=pr, payload_size=ps, heartbeat_port=_free_port(), quiet=True)
+        th, out = _run_server(srv)
+        ver = cl.GpuVerifier([0])
+        rc, pw = cl.connect_to_server("127.0.0.1", srv.address[1], "gpu", ver, quiet=True)
+        ver.close()
+        th.join(10)
+        assert (rc, pw) == (0, d["password"]), name
+        assert out["pw"] == d["password"]
