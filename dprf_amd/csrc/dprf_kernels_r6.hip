@@ -339,6 +339,15 @@ DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
     }
 }
 
+#ifdef DPRF_R6_TIMING
+/* debug builds (-DDPRF_R6_TIMING): per-wave cycle split of the round loop, printed for a few workgroups */
+#define R6T_DECL unsigned long long t_bar = 0, t_fam = 0, t_work = 0, t_x = __builtin_readcyclecounter();
+#define R6T_MARK(acc) { unsigned long long t_y = __builtin_readcyclecounter(); acc += t_y - t_x; t_x = t_y; }
+#else
+#define R6T_DECL
+#define R6T_MARK(acc)
+#endif
+
 template <int MODE>
 __global__ void __launch_bounds__(R6_MAX_SLOTS, 1)     /* 12 waves/CU: <= 168 VGPRs */
 k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
@@ -355,8 +364,11 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     __syncthreads();
 
     r6_start<MODE>(e, p, cs, R, stop_on_first, sh, slot_lds(patbase, pat_words, tid, lane), tid);
+    R6T_DECL
     for (;;) {
+        R6T_MARK(t_work)
         __syncthreads();
+        R6T_MARK(t_bar)
         /* phase 1: family of my own slot; rank within its class by an LDS atomic */
         uint32_t cls = R6_CLASSES - 1, hsel = 0;
         if (sh->cand[tid] != R6_IDLE) {
@@ -365,14 +377,18 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             cls = (hsel ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
         }
         const uint32_t rank = atomicAdd(&sh->hist[cls], 1u);
+        R6T_MARK(t_fam)
         __syncthreads();
+        R6T_MARK(t_bar)
         if (sh->hist[R6_CLASSES - 1] == nslots) break;             /* no slot has a candidate: uniform exit */
         uint32_t pos = rank;
 #pragma unroll
         for (uint32_t k = 0; k < R6_CLASSES - 1; k++) pos += k < cls ? sh->hist[k] : 0u;
         sh->order[pos] = (uint16_t)tid;
         sh->state[tid] |= hsel << 30;          /* round counter (bits 16..29) < 2^14 */
+        R6T_MARK(t_fam)
         __syncthreads();
+        R6T_MARK(t_bar)
         if (tid < 8) sh->hist[tid] = 0u;
         /* phase 2: the round of slot order[tid] */
         const uint32_t slot = sh->order[tid];
@@ -401,6 +417,10 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             sh->state[slot] = len | (bs << 8) | (i << 16);
         }
     }
+#ifdef DPRF_R6_TIMING
+    if (lane == 0 && blockIdx.x < 2)
+        printf("r6 timing wg %u wave %u: work %llu fam %llu barrier %llu\n", blockIdx.x, tid >> 6, t_work, t_fam, t_bar);
+#endif
     if (tid == 0 && sh->done) atomicAdd(&R->evaluated, (unsigned long long)sh->done);
 }
 
