@@ -27,11 +27,14 @@
 #include "dprf_params.h"
 #include "dprf_launch.h"
 
-/* Te0 replicated 64x: entry x, copy c at byte 256*x + 4*c.  Lane l reads copy l, so the 32 lanes of a
- * ds_read_b32 group hit 32 different banks whatever the indices (conflict-free), and the address of
- * byte k of a state word is ONE v_perm: byte 1 <- byte k of the word, byte 0 <- 4*lane, bytes 2-3 <- 0. */
-#define R6_TE_COPIES 64
-#define R6_TE_BYTES (R6_TE_COPIES * 1024)
+/* Te0 replicated 32x: entry x, copy c at byte 256*x + 4*c (c < 32).  Lane l reads copy l%32, so each
+ * 32-lane group of a ds_read_b32 ({0-31}, {32-63}: MI355X_MICROARCH.md LDS table) hits 32 different banks
+ * whatever the indices (conflict-free), and the address of byte k of a state word is ONE v_perm: byte 1
+ * <- byte k of the word, byte 0 <- 4*(lane%32), bytes 2-3 <- 0.  Bytes 128..255 of every row are free:
+ * they hold the periods of 32-slot groups (slot_lds), so the 64 KiB the addressing needs is not lost. */
+#define R6_TE_ROW_BYTES 256
+#define R6_TE_COPIES 32
+#define R6_TE_BYTES (256 * R6_TE_ROW_BYTES)
 
 DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
     uint32_t t = __umulhi(n, m);
@@ -42,10 +45,17 @@ DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
  * the whole address */
 __shared__ __attribute__((aligned(16))) uint32_t r6_te[R6_TE_BYTES / 4];
 
+/* LDS pointers from 32-bit LDS byte addresses (address space 3: ds_* instructions, no flat pointers) */
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+DEVI lds_u8 *L8(uint32_t a) { return (lds_u8 *)(size_t)a; }
+DEVI lds_u32 *L32(uint32_t a) { return (lds_u32 *)(size_t)a; }
+DEVI uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(const lds_u8 *)p; }
+
 struct r6_lds {
-    uint8_t *pat;              /* [pat_words][64 lanes] words of the wave that owns the slot */
+    uint32_t pat;              /* LDS byte address of the slot's group: rows of 256 bytes */
     uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
-    uint32_t lanec;            /* 4 * (thread lane): this thread's Te0 copy */
+    uint32_t lanec;            /* 4 * (thread lane % 32): this thread's Te0 copy */
 };
 
 /* Te0[byte k of v] */
@@ -176,7 +186,7 @@ DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8
     for (int j = 8; j < 16; j++) K[j] = 0u;
     /* pw at the head of the period (word-aligned; bytes past len are overwritten by K) */
 #pragma unroll
-    for (int j = 0; j < DPRF_SLOT_WORDS; j++) *(uint32_t *)(S.pat + (((uint32_t)j << 8) | S.lanebase)) = w[j];
+    for (int j = 0; j < DPRF_SLOT_WORDS; j++) *L32(S.pat + (((uint32_t)j << 8) | S.lanebase)) = w[j];
     return len;
 }
 
@@ -187,17 +197,17 @@ DEVI void r6_store_k(const r6_lds &S, uint32_t len, uint32_t bs, const uint32_t 
     for (int k = 0; k < 64; k++) {
         if ((uint32_t)k < bs) {
             const uint32_t b = (K[k >> 2] >> (24 - 8 * (k & 3))) & 0xffu;
-            S.pat[pat_addr(len + k, S.lanebase)] = (uint8_t)b;
+            *L8(S.pat + pat_addr(len + k, S.lanebase)) = (uint8_t)b;
         }
     }
     const uint32_t Lp = len + bs;
-    for (uint32_t k = 0; k < 16; k++) S.pat[pat_addr(Lp + k, S.lanebase)] = S.pat[pat_addr(k, S.lanebase)];
+    for (uint32_t k = 0; k < 16; k++) *L8(S.pat + pat_addr(Lp + k, S.lanebase)) = *L8(S.pat + pat_addr(k, S.lanebase));
 }
 
 /* Four BE words starting at byte o of the slot's period (one v_perm per word). */
 DEVI void r6_read16(const r6_lds &S, uint32_t o, uint32_t v[4]) {
     const uint32_t sel = 0x00010203u + (o & 3u) * 0x01010101u;
-    const uint32_t *col = (const uint32_t *)(S.pat + (((o >> 2) << 8) | S.lanebase));
+    const lds_u32 *col = L32(S.pat + (((o >> 2) << 8) | S.lanebase));
     uint32_t lw[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) lw[k] = col[k * 64];
@@ -292,33 +302,57 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
     return prev[3] & 0xffu;
 }
 
-/* Slots and classes.  One workgroup per CU holds up to R6_MAX_SLOTS candidates ("slots"); everything a
- * slot needs between rounds is in LDS: its period (pw || K[0:bs] || wrap) in a column of the pattern area,
- * and a state word.  Each round, every thread first finds the hash family of its own slot (one AES
- * block), the slots are counting-sorted by class = (family is SHA-256 ? 0 : 3) + (bs - 32) / 16 (the data
- * length is 64 x (len + bs)), and thread t then runs the round of the t-th slot in class order.  Waves
- * thereby see one hash family and one trip count (up to the class boundaries) instead of running SHA-256
- * and SHA-384/512 predicated and to the longest period in the wave; slots with no candidate left sort
- * last, so idle waves skip the round whole.  A finished slot takes the next candidate of the launch from
- * a global cursor, so no workgroup idles while another still has work. */
-#define R6_MAX_SLOTS 768
+/* Slots, classes and batches.  One workgroup per CU (12 waves) holds up to R6_MAX_SLOTS candidates
+ * ("slots") -- more slots than lanes; everything a slot needs between rounds is in LDS: its period
+ * (pw || K[0:bs] || wrap) in a column of a pattern area, a state word and its candidate number.  Each
+ * interval:
+ *  1. every live slot finds the hash family of its next round (one AES block) and is counting-sorted by
+ *     class = (family is SHA-256 ? 0 : 3) + (bs - 32) / 16 (the data length is 64 x (len + bs));
+ *  2. each family's sorted slots are cut into batches of 64 consecutive slots (one family per batch, the
+ *     trip count of a batch is that of its longest period), costed per 64-byte unit of their family and
+ *     listed costliest first;
+ *  3. each wave repeatedly takes the next batch of that list (an LDS counter) and runs one round of it
+ *     (greedy list scheduling: a wave that runs faster because fewer waves share its SIMD takes more),
+ *     then all meet at the barrier.
+ * With slots = lanes and one batch per wave (the previous schedule), waves of cheap classes sat 37 % of
+ * the time at the barrier (profiles/r6_round_timing_r01.txt); with ~1.6x as many slots as lanes the
+ * list scheduling evens the waves' loads.  A finished slot takes the next candidate of the launch from a global
+ * cursor, so no workgroup idles while another still has work.
+ *
+ * Pattern areas: slots [0, te_slots) live in the free upper halves of the Te0 rows in groups of 32
+ * (column 128 + 4*(slot%32)), the rest in the dynamic area in groups of 64 (column 4*(slot%64)); rows are
+ * 256 bytes apart in both, so r6_read16 and friends see one layout. */
+#define R6_LANES 768
+#define R6_MAX_SLOTS 1280
 #define R6_CLASSES 7                    /* 6 live classes + "no candidate" */
 #define R6_IDLE 0xffffffffu
+#define R6_MAX_BATCHES (R6_MAX_SLOTS / 64 + 2)
 
 struct r6_shared {
     uint32_t hist[8];
     uint32_t done;                      /* candidates finished by this workgroup */
-    uint32_t flag;
+    uint32_t nslots, te_slots, pad;
+    uint16_t bstart[R6_MAX_BATCHES];    /* batch b = order[bstart[b] .. bstart[b] + bsize[b]) */
+    uint8_t bsize[R6_MAX_BATCHES];
+    uint32_t bcost[R6_MAX_BATCHES];
+    uint32_t nbatches, next_batch;      /* batches of this interval; the next one a wave takes */
+    uint8_t ids[R6_MAX_BATCHES];        /* batch ids, costliest first */
     uint32_t state[R6_MAX_SLOTS];       /* len | bs << 8 | round << 16 | family << 30 */
     uint32_t cand[R6_MAX_SLOTS];        /* candidate offset within the launch, R6_IDLE when none */
-    uint16_t order[R6_MAX_SLOTS];       /* slot run by thread t this round */
+    uint16_t order[R6_MAX_SLOTS];       /* slots sorted by class */
 };
 
-DEVI r6_lds slot_lds(uint8_t *patbase, uint32_t pat_words, uint32_t slot, uint32_t lane) {
+DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, uint32_t slot, uint32_t lane) {
     r6_lds S;
-    S.pat = patbase + (size_t)(slot >> 6) * pat_words * 256u;
-    S.lanebase = (slot & 63u) << 2;
-    S.lanec = lane << 2;
+    if (slot < te_slots) {
+        S.pat = lds_addr(r6_te) + (slot >> 5) * pat_words * 256u;
+        S.lanebase = 128u + ((slot & 31u) << 2);
+    } else {
+        const uint32_t t = slot - te_slots;
+        S.pat = patbase + (t >> 6) * pat_words * 256u;
+        S.lanebase = (t & 63u) << 2;
+    }
+    S.lanec = (lane & 31u) << 2;
     return S;
 }
 
@@ -339,9 +373,14 @@ DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
     }
 }
 
+/* cost of one round of a batch whose longest period is Lp, in units of ~1/64 issue slot:
+ * per 64-byte unit 4 AES blocks + 1 SHA-256c (4 x 478 + 2446) or half a SHA-512c (4 x 478 + 3186) */
+DEVI uint32_t r6_cost(uint32_t family_group, uint32_t Lp) { return Lp * (family_group ? 5098u : 4358u); }
+
 #ifdef DPRF_R6_TIMING
 /* debug builds (-DDPRF_R6_TIMING): per-wave cycle split of the round loop, printed for a few workgroups */
-#define R6T_DECL unsigned long long t_bar = 0, t_fam = 0, t_work = 0, t_x = __builtin_readcyclecounter();
+#define R6T_DECL unsigned long long t_bar = 0, t_fam = 0, t_work = 0, t_x = __builtin_readcyclecounter(); \
+    unsigned long long t_cyc[2] = {0, 0}, t_units[2] = {0, 0}, t_nb[2] = {0, 0};
 #define R6T_MARK(acc) { unsigned long long t_y = __builtin_readcyclecounter(); acc += t_y - t_x; t_x = t_y; }
 #else
 #define R6T_DECL
@@ -349,88 +388,155 @@ DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
 #endif
 
 template <int MODE>
-__global__ void __launch_bounds__(R6_MAX_SLOTS, 1)     /* 12 waves/CU: <= 168 VGPRs */
+__global__ void __launch_bounds__(R6_LANES, 1)     /* 12 waves/CU: <= 168 VGPRs */
 k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
-         uint32_t stop_on_first, uint32_t pat_words) {
+         uint32_t stop_on_first, uint32_t pat_words, uint32_t nslots, uint32_t te_slots) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];               /* after r6_te */
     uint8_t *cs = (uint8_t *)smem;                                              /* 256 B */
     r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
-    uint8_t *patbase = (uint8_t *)smem + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, nslots = blockDim.x;
-    for (uint32_t k = tid; k < R6_TE_BYTES / 4; k += nslots) r6_te[k] = T->te0[k / R6_TE_COPIES];
-    for (uint32_t k = tid; k < 64; k += nslots) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
+    const uint32_t patbase = lds_addr(smem) + 256u + (uint32_t)((sizeof(r6_shared) + 15) / 16 * 16);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, nthr = blockDim.x;
+    /* Te0 copies into bytes 0..127 of each row; the upper halves are slot periods */
+    for (uint32_t k = tid; k < 256u * R6_TE_COPIES; k += nthr)
+        r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = T->te0[k >> 5];
+    for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     if (tid < 8) sh->hist[tid] = 0u;
     if (tid == 0) sh->done = 0u;
     __syncthreads();
 
-    r6_start<MODE>(e, p, cs, R, stop_on_first, sh, slot_lds(patbase, pat_words, tid, lane), tid);
+    for (uint32_t sl = tid; sl < nslots; sl += nthr)
+        r6_start<MODE>(e, p, cs, R, stop_on_first, sh, slot_lds(patbase, pat_words, te_slots, sl, lane), sl);
     R6T_DECL
     for (;;) {
         R6T_MARK(t_work)
         __syncthreads();
         R6T_MARK(t_bar)
-        /* phase 1: family of my own slot; rank within its class by an LDS atomic */
-        uint32_t cls = R6_CLASSES - 1, hsel = 0;
-        if (sh->cand[tid] != R6_IDLE) {
-            const uint32_t st = sh->state[tid];
-            hsel = r6_family(slot_lds(patbase, pat_words, tid, lane), st & 0xffu);
-            cls = (hsel ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
+        /* 1. family of each slot this thread looks after; rank within its class by an LDS atomic */
+        uint32_t mycls[2], myrank[2], myh[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t sl = tid + (uint32_t)q * nthr;
+            mycls[q] = R6_CLASSES - 1; myh[q] = 0; myrank[q] = 0;
+            if (sl < nslots) {
+                if (sh->cand[sl] != R6_IDLE) {
+                    const uint32_t st = sh->state[sl];
+                    myh[q] = r6_family(slot_lds(patbase, pat_words, te_slots, sl, lane), st & 0xffu);
+                    mycls[q] = (myh[q] ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
+                }
+                myrank[q] = atomicAdd(&sh->hist[mycls[q]], 1u);
+            }
         }
-        const uint32_t rank = atomicAdd(&sh->hist[cls], 1u);
         R6T_MARK(t_fam)
         __syncthreads();
         R6T_MARK(t_bar)
         if (sh->hist[R6_CLASSES - 1] == nslots) break;             /* no slot has a candidate: uniform exit */
-        uint32_t pos = rank;
 #pragma unroll
-        for (uint32_t k = 0; k < R6_CLASSES - 1; k++) pos += k < cls ? sh->hist[k] : 0u;
-        sh->order[pos] = (uint16_t)tid;
-        sh->state[tid] |= hsel << 30;          /* round counter (bits 16..29) < 2^14 */
-        R6T_MARK(t_fam)
-        __syncthreads();
-        R6T_MARK(t_bar)
-        if (tid < 8) sh->hist[tid] = 0u;
-        /* phase 2: the round of slot order[tid] */
-        const uint32_t slot = sh->order[tid];
-        if (sh->cand[slot] == R6_IDLE) continue;
-        const r6_lds S = slot_lds(patbase, pat_words, slot, lane);
-        const uint32_t st = sh->state[slot];
-        const uint32_t len = st & 0xffu, hs = st >> 30;
-        uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
-        uint32_t K[16];
-        const uint32_t last = r6_round(S, len, bs, hs, K);
-        i++;
-        if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
-            bool ok = true;
+        for (int q = 0; q < 2; q++) {
+            const uint32_t sl = tid + (uint32_t)q * nthr;
+            if (sl < nslots) {
+                uint32_t pos = myrank[q];
 #pragma unroll
-            for (int k = 0; k < 8; k++) ok = ok && K[k] == p.u[k];
-            if (ok) {
-                const unsigned long long idx = e.start + sh->cand[slot];
-                uint32_t h = atomicAdd(&R->nhits, 1u);
-                if (h < cap) R->hits[h] = idx;
-                atomicMin(&R->first, idx);
-                if (stop_on_first) atomicExch(&R->stop, 1u);
+                for (uint32_t k = 0; k < R6_CLASSES - 1; k++) pos += k < mycls[q] ? sh->hist[k] : 0u;
+                sh->order[pos] = (uint16_t)sl;
+                sh->state[sl] |= myh[q] << 30;          /* round counter (bits 16..29) < 2^14 */
             }
-            atomicAdd(&sh->done, 1u);
-            r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
-        } else {
-            sh->state[slot] = len | (bs << 8) | (i << 16);
+        }
+        /* 2. batches of 64 within each family group, longest-processing-time-first onto the waves */
+        if (tid == 0) {
+            uint32_t nb = 0, base = 0;
+            for (uint32_t fg = 0; fg < 2; fg++) {
+                uint32_t n = sh->hist[3 * fg] + sh->hist[3 * fg + 1] + sh->hist[3 * fg + 2];
+                for (uint32_t o = 0; o < n; o += 64u) {
+                    const uint32_t sz = n - o < 64u ? n - o : 64u;
+                    /* longest period of the batch: its last slot (sorted by bs within the family) */
+                    const uint32_t stl = sh->state[sh->order[base + o + sz - 1]];
+                    sh->bstart[nb] = (uint16_t)(base + o);
+                    sh->bsize[nb] = (uint8_t)sz;
+                    sh->bcost[nb] = r6_cost(fg, (stl & 0xffu) + ((stl >> 8) & 0xffu));
+                    nb++;
+                }
+                base += n;
+            }
+            /* sort batch ids by cost, descending (insertion sort, <= 22 entries) */
+            for (uint32_t b = 0; b < nb; b++) {
+                uint32_t k = b;
+                const uint32_t cb = sh->bcost[b];
+                while (k > 0 && sh->bcost[sh->ids[k - 1]] < cb) { sh->ids[k] = sh->ids[k - 1]; k--; }
+                sh->ids[k] = (uint8_t)b;
+            }
+            sh->nbatches = nb;
+            sh->next_batch = 0;
+        }
+        __syncthreads();
+        if (tid < 8) sh->hist[tid] = 0u;
+        /* 3. rounds of batches, costliest first, each wave taking the next one when it is free */
+        const uint32_t nb = sh->nbatches;
+        for (;;) {
+            /* the wave takes the costliest batch nobody has taken yet (greedy list scheduling in
+             * cost order: waves that run faster -- fewer co-resident waves on their SIMD -- take more) */
+            uint32_t kk = 0;
+            if (lane == 0) kk = atomicAdd(&sh->next_batch, 1u);
+            kk = __builtin_amdgcn_readfirstlane(kk);
+            if (kk >= nb) break;
+            const uint32_t b = sh->ids[kk];
+#ifdef DPRF_R6_TIMING
+            const unsigned long long tb0 = __builtin_readcyclecounter();
+            if (lane == 0) {
+                const uint32_t stl = sh->state[sh->order[sh->bstart[b] + sh->bsize[b] - 1]];
+                t_units[stl >> 30 ? 1 : 0] += (stl & 0xffu) + ((stl >> 8) & 0xffu);
+                t_nb[stl >> 30 ? 1 : 0] += 1;
+            }
+            struct tb_guard { unsigned long long t0, *acc; uint32_t on;
+                __device__ ~tb_guard() { if (on) *acc += __builtin_readcyclecounter() - t0; } };
+            tb_guard tg{tb0, &t_cyc[sh->state[sh->order[sh->bstart[b] + sh->bsize[b] - 1]] >> 30 ? 1 : 0], lane == 0};
+#endif
+            if (lane >= sh->bsize[b]) continue;
+            const uint32_t slot = sh->order[sh->bstart[b] + lane];
+            const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, lane);
+            const uint32_t st = sh->state[slot];
+            const uint32_t len = st & 0xffu, hs = st >> 30;
+            uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
+            uint32_t K[16];
+            const uint32_t last = r6_round(S, len, bs, hs, K);
+            i++;
+            if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
+                bool ok = true;
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) ok = ok && K[kk] == p.u[kk];
+                if (ok) {
+                    const unsigned long long idx = e.start + sh->cand[slot];
+                    uint32_t h = atomicAdd(&R->nhits, 1u);
+                    if (h < cap) R->hits[h] = idx;
+                    atomicMin(&R->first, idx);
+                    if (stop_on_first) atomicExch(&R->stop, 1u);
+                }
+                atomicAdd(&sh->done, 1u);
+                r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
+            } else {
+                sh->state[slot] = len | (bs << 8) | (i << 16);
+            }
         }
     }
 #ifdef DPRF_R6_TIMING
     if (lane == 0 && blockIdx.x < 2)
-        printf("r6 timing wg %u wave %u: work %llu fam %llu barrier %llu\n", blockIdx.x, tid >> 6, t_work, t_fam, t_bar);
+        printf("r6 timing wg %u wave %u: work %llu fam %llu barrier %llu | sha256 batches %llu units %llu cyc %llu | sha512 batches %llu units %llu cyc %llu\n",
+               blockIdx.x, tid >> 6, t_work, t_fam, t_bar, t_nb[0], t_units[0], t_cyc[0], t_nb[1], t_units[1], t_cyc[1]);
 #endif
     if (tid == 0 && sh->done) atomicAdd(&R->evaluated, (unsigned long long)sh->done);
 }
 
-/* Waves per workgroup: as many of the 12 the VGPR budget allows as fit next to the 64 KiB table. */
-static uint32_t r6_waves(uint32_t pat_words) {
+/* Slot capacity of one workgroup: 32-slot groups in the upper halves of the Te0 rows, then 64-slot groups
+ * in the dynamic LDS left next to the table and the shared block (160 KiB per workgroup). */
+static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots, size_t *shm) {
     const size_t fixed = R6_TE_BYTES + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
-    const size_t per_wave = (size_t)pat_words * 256u;
-    uint32_t nw = (uint32_t)((160u * 1024u - fixed) / per_wave);
-    if (nw > R6_MAX_SLOTS / 64) nw = R6_MAX_SLOTS / 64;
-    return nw >= 4 ? nw & ~3u : nw;
+    const uint32_t te_groups = 256u / pat_words;
+    uint32_t te = te_groups * 32u;
+    uint32_t dyn = (uint32_t)((160u * 1024u - fixed) / ((size_t)pat_words * 256u)) * 64u;
+    if (te > R6_MAX_SLOTS) te = R6_MAX_SLOTS;
+    if (te + dyn > R6_MAX_SLOTS) dyn = (R6_MAX_SLOTS - te) / 64u * 64u;
+    *te_slots = te;
+    *nslots = te + dyn;
+    *shm = 256 + (sizeof(r6_shared) + 15) / 16 * 16 + (size_t)(dyn / 64u) * pat_words * 256u;   /* + static r6_te */
 }
 
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
@@ -438,9 +544,13 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     const uint32_t lmax = e.mode == 0 ? e.pwlen : 4u * DPRF_SLOT_WORDS;
     /* period (lmax + 64) + 16 wrap bytes, + 4 words read past the last block start */
     const uint32_t pat_words = (lmax + 64u + 16u + 3u) / 4u + 1u;
-    const uint32_t nw = r6_waves(pat_words);
-    if (nw == 0) return hipErrorInvalidValue;
-    const size_t shm = 256 + (sizeof(r6_shared) + 15) / 16 * 16 + (size_t)nw * pat_words * 256u;   /* + static r6_te */
+    uint32_t nslots = 0, te_slots = 0;
+    size_t shm = 0;
+    r6_capacity(pat_words, &nslots, &te_slots, &shm);
+    if (nslots < 64) return hipErrorInvalidValue;
+    /* lanes: 12 waves, or fewer when there are fewer slots */
+    uint32_t lanes = (nslots / 64u) * 64u;
+    if (lanes > R6_LANES) lanes = R6_LANES;
     static bool attr_set[2] = {false, false};
     /* the work cursor restarts at 0 for every launch (stream-ordered before the kernel) */
     hipError_t me = hipMemsetAsync(&R->cursor, 0, sizeof(uint32_t), s);
@@ -450,15 +560,14 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
     /* one workgroup per CU; a launch smaller than the slots it would open uses fewer workgroups */
-    const uint32_t slots = nw * 64u;
-    uint32_t grid = (e.count + slots - 1) / slots;
+    uint32_t grid = (e.count + nslots - 1) / nslots;
     if (grid > (uint32_t)ncu) grid = (uint32_t)ncu;
     if (e.mode == 0) {
         if (!attr_set[0]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[0] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(slots), shm, s, e, p, T, R, cap, stop, pat_words);
+        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
     } else {
         if (!attr_set[1]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[1] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(slots), shm, s, e, p, T, R, cap, stop, pat_words);
+        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
     }
     return hipGetLastError();
 }
