@@ -19,7 +19,8 @@ candidates go to libdprf.so in batches, one candidate per GPU lane.  Differences
 * a verifier error is raised as :class:`dprf_amd._lib.DprfError`, never reported as found (the reference
   counts any non-zero exit as a hit, :140; Appendix B.6).
 * optional keyword arguments ``charset`` (default lowercase a-z, Python 2 ``string.lowercase`` in the C
-  locale) and ``devices`` (default: every visible gfx950 GPU).
+  locale), ``devices`` (default: every visible gfx950 GPU) and ``checkpoint`` (a resumable cursor file
+  for range mode, :class:`Checkpoint`).
 """
 import argparse
 import re
@@ -37,7 +38,7 @@ DUMMY = "_dummy"
 ROUND_PER_DEVICE = 1 << 24      # candidates per device between stop checks in range mode
 
 
-def init(stream, password_range, passwords, charset=LOWERCASE, devices=None):
+def init(stream, password_range, passwords, charset=LOWERCASE, devices=None, checkpoint=None):
     # The common entry point (brute_force.py:39-57)
     if not password_range and not passwords:
         raise ValueError('Need to provide a password range to generate or a list of passwords.')
@@ -49,7 +50,8 @@ def init(stream, password_range, passwords, charset=LOWERCASE, devices=None):
 
     try:
         if password_range and not passwords:
-            return init_rangebased_brute_force(input_data, password_range, charset=charset, devices=devices)
+            return init_rangebased_brute_force(input_data, password_range, charset=charset, devices=devices,
+                                               checkpoint=checkpoint)
         if passwords and not password_range:
             return init_listbased_brute_force(input_data, passwords, devices=devices)
     except KeyboardInterrupt:
@@ -76,21 +78,65 @@ def _report(found_pw, n, t0):
         print("Correct password is '" + found_pw + "'")
 
 
-def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, devices=None):
+class Checkpoint:
+    """Resumable shard cursor for range mode (an extension; the reference has none).  A JSON file records
+    which search it belongs to (SHA-256 of the verifier stream, charset, length) and the keyspace index
+    below which every candidate has been verified; it is rewritten atomically after every round, so an
+    interrupted run restarts at its last completed round."""
+
+    def __init__(self, path, input_data, charset, pwlen):
+        import hashlib
+        self.path = path
+        self.key = {"stream_sha256": hashlib.sha256("*".join(map(str, input_data)).encode()).hexdigest(),
+                    "charset": charset, "pwlen": int(pwlen)}
+
+    def load(self):
+        """(next index, found password or None) recorded for this search; (0, None) when there is none."""
+        import json
+        import os
+        if not self.path or not os.path.exists(self.path):
+            return 0, None
+        with open(self.path) as f:
+            d = json.load(f)
+        if any(d.get(k) != v for k, v in self.key.items()):
+            raise ValueError("checkpoint %s belongs to a different search" % self.path)
+        return int(d["next_index"]), d.get("found")
+
+    def save(self, next_index, found=None):
+        import json
+        import os
+        if not self.path:
+            return
+        tmp = self.path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(dict(self.key, next_index=int(next_index), found=found), f)
+        os.replace(tmp, self.path)
+
+
+def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, devices=None, checkpoint=None):
     """charset^password_range in product order, plus "_dummy" (brute_force.py:60-79, :199-219).
 
     Multi-GPU: each round gives every device a contiguous slice of one contiguous block of the keyspace,
     so after a round every index below the round's end has been verified and the lowest hit of the
-    first round that has one is the lowest hit overall."""
+    first round that has one is the lowest hit overall.  checkpoint: path of a resumable cursor file
+    (:class:`Checkpoint`)."""
+    cp = Checkpoint(checkpoint, input_data, charset, password_range)
+    done, prior = cp.load()
+    if prior is not None:
+        print("Checkpoint: search already finished, password '%s'" % prior)
+        return 1, prior
     ctxs = _contexts(input_data, devices)
     t0 = time.time()
     try:
-        hits, _, _ = ctxs[0].verify_list([DUMMY], stop_on_first=True, cap=1)
-        if hits:
-            _report(DUMMY, 1, t0)
-            return 1, DUMMY
+        if done == 0:
+            hits, _, _ = ctxs[0].verify_list([DUMMY], stop_on_first=True, cap=1)
+            if hits:
+                cp.save(0, DUMMY)
+                _report(DUMMY, 1, t0)
+                return 1, DUMMY
+        else:
+            print("Checkpoint: resuming at index %d" % done)
         space = len(charset) ** password_range
-        done = 0
         found = None
         while done < space and found is None:
             block = min(space - done, ROUND_PER_DEVICE * len(ctxs))
@@ -112,6 +158,7 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
                 idx = min(firsts)
                 found = _index_to_password(idx, charset, password_range)
             done += block
+            cp.save(done, found)
         _report(found, done + 1, t0)
         return (1, found) if found is not None else (0, DEFAULT_PASSWORD)
     finally:
@@ -223,6 +270,7 @@ def main(argv=None):
     parser.add_argument("-pr", "--passwordrange", type=int, help="password range to brute-force (i.e., 2 -> aa..zz)")
     parser.add_argument("--charset", default=LOWERCASE, help="candidate alphabet (default a-z)")
     parser.add_argument("--devices", default=None, help="comma-separated GPU ordinals (default: all)")
+    parser.add_argument("--checkpoint", default=None, help="resumable cursor file (written after every round)")
     args = parser.parse_args(argv)
 
     stream = get_verification_data(args.document_type, args.filename)
@@ -230,7 +278,7 @@ def main(argv=None):
         sys.exit(0)
     devices = [int(x) for x in args.devices.split(",")] if args.devices else None
     found, password = init(stream, args.passwordrange if args.passwordrange else 8, None,
-                           charset=args.charset, devices=devices)
+                           charset=args.charset, devices=devices, checkpoint=args.checkpoint)
     if not found:
         print("Password is not in brute-forced space.")
     return found, password

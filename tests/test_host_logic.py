@@ -1,6 +1,7 @@
 """Host-side logic of the brute_force counterpart (no GPU): field split, tag regex, argument checks,
 enumeration order, parsers."""
 import itertools
+import json
 
 import pytest
 
@@ -89,3 +90,48 @@ def test_get_verification_data_uses_engine_parser_modes(streams, capsys):
     assert bf.get_verification_data("2", REF_FILES + "/odt/password.odt") == streams["odt_testdoc_e"]["stream"]
     assert bf.get_verification_data("3", REF_FILES + "/pdf/password_1.7_v4_r4.pdf") == streams["pdf_testdoc_r4"]["stream"]
     assert bf.get_verification_data("1", REF_FILES + "/ms/password.docx") == streams["office_testdoc"]["stream"]
+
+
+class _OracleCtx:
+    """Stand-in for _lib.Context backed by the oracle (test infrastructure), recording the ranges asked."""
+
+    def __init__(self, oracle, stream, log, fail_at=None):
+        self.c = oracle.Ctx(stream)
+        self.log = log
+        self.fail_at = fail_at
+
+    def verify_list(self, passwords, stop_on_first=False, cap=1 << 16):
+        h = [i for i, p in enumerate(passwords) if self.c.verify(p.encode())]
+        return h[:cap], len(h), {}
+
+    def search_range(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
+        if self.fail_at is not None and start >= self.fail_at:
+            raise KeyboardInterrupt
+        self.log.append((start, count))
+        h, n = self.c.search_range(charset, pwlen, start, count)
+        return h[:cap], n, {}            # absolute keyspace indices, like _lib.Context
+
+    def close(self):
+        pass
+
+
+def test_range_checkpoint_resumes_where_it_stopped(streams, oracle, tmp_path, monkeypatch):
+    d = streams["pdf_synth_r5_cat"]
+    fields = bf.parse_verification_data(d["stream"])
+    monkeypatch.setattr(bf, "ROUND_PER_DEVICE", 1000)
+    cp = str(tmp_path / "cursor.json")
+    want = bf.LOWERCASE.index("c") * 676 + bf.LOWERCASE.index("a") * 26 + bf.LOWERCASE.index("t")
+    log1 = []
+    monkeypatch.setattr(bf, "_contexts", lambda inp, dev: [_OracleCtx(oracle, d["stream"], log1, fail_at=1000)])
+    with pytest.raises(KeyboardInterrupt):
+        bf.init_rangebased_brute_force(fields, 3, checkpoint=cp)
+    assert log1 == [(0, 1000)]
+    assert json.load(open(cp))["next_index"] == 1000
+    log2 = []
+    monkeypatch.setattr(bf, "_contexts", lambda inp, dev: [_OracleCtx(oracle, d["stream"], log2)])
+    assert bf.init_rangebased_brute_force(fields, 3, checkpoint=cp) == (1, "cat")
+    assert log2[0] == (1000, 1000) and log2[-1][0] <= want < log2[-1][0] + log2[-1][1]
+    # finished searches answer from the checkpoint; a different search refuses it
+    assert bf.init_rangebased_brute_force(fields, 3, checkpoint=cp) == (1, "cat")
+    with pytest.raises(ValueError):
+        bf.init_rangebased_brute_force(fields, 4, checkpoint=cp)
