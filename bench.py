@@ -119,6 +119,40 @@ def _cpu_worker(job):
     return n
 
 
+def _popen_worker(job):
+    """One worker of the reference's process model: Popen + wait of the reference verifier executable per
+    candidate (brute_force.py:123-140, argv of :163-197), candidates t, t+P, ... until the deadline."""
+    fields, charset, pwlen, t, procs, deadline = job
+    import subprocess
+    from dprf_amd.brute_force import _index_to_password
+    sys.path.insert(0, os.path.join(HERE, "tests", "golden"))
+    from make_golden import ENV, ref_argv
+    n, i = 0, t
+    while time.time() < deadline:
+        subprocess.run(ref_argv(fields, _index_to_password(i, charset, pwlen)), env=ENV,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        n += 1
+        i += procs
+    return n
+
+
+def reference_process_model(fields, charset, pwlen, seconds=2.0, procs=4):
+    """The reference engine's own cost structure: 4 worker processes (brute_force.py:70-73), one fork/exec
+    of the compiled reference verifier per candidate.  Python 3 drives it (there is no Python 2.7 here)."""
+    import multiprocessing as mp
+    exe = os.path.join(HERE, "oracle", "_ref", {"office": "msoffcrypto", "odt": "odt", "pdf": "pdf"}[fields[0]])
+    if not os.path.exists(exe):
+        return None
+    with mp.get_context("spawn").Pool(procs) as pool:
+        t0 = time.time()
+        counts = pool.map(_popen_worker, [(fields, charset, pwlen, t, procs, t0 + seconds) for t in range(procs)])
+        dt = time.time() - t0
+    n = sum(counts)
+    return {"value": n / dt, "unit": "candidates/s", "cores": procs, "kind": "reference",
+            "sample": "%d candidates in %.1f s: brute_force.py's 4 worker processes, one Popen of the reference "
+                      "verifier executable (compiled from /root/reference) per candidate" % (n, dt)}
+
+
 def cpu_baseline(fields, charset, pwlen, seconds=1.5, procs=None):
     """The reference's verify() on the host cores, one worker PROCESS per core (the reference's own process
     model, brute_force.py:70-73, minus its per-candidate fork/exec), for a bounded time over the first
@@ -225,6 +259,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(fields, cs, pwlen, seconds=args.cpu_seconds)
+        pm = reference_process_model(fields, cs, pwlen)
+        if pm:
+            cpu["reference_process_model"] = pm
         log("cpu baseline:", cpu)
 
     ctx = _lib.Context(fields, device=local)
