@@ -294,13 +294,59 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
     for (int k = 0; k < 8; k++) keys[(size_t)k * e.count + g] = key[k];
 }
 
-__global__ void __launch_bounds__(256)
+/* The 64 AES-256 block decryptions per candidate read Td0 14,336 times.  A single 1 KiB Td0 puts
+ * random indices of 32 lanes on 32 banks (~3.5-way conflicts: 65 % of this kernel's cycles were bank
+ * conflicts, profiles/prof_odt_r01.json).  Here row x of a 64 KiB table holds Td0[x] in 32 dword copies
+ * (bytes 0..127, lane l reads copy l%32) and Si[x] in 32 dword copies (bytes 128..255): every lookup is
+ * conflict-free and its address is ONE v_perm of the state byte and the lane's copy offset. */
+#define ODT_TD_ROW 256
+__shared__ __attribute__((aligned(16))) uint32_t odt_td[256 * ODT_TD_ROW / 4];
+
+template <int K>
+DEVI uint32_t tdrep(uint32_t v, uint32_t lanec) {
+    const uint32_t a = __builtin_amdgcn_perm(v, lanec, 0x0c0c0000u | ((4u + K) << 8));
+    return *(const uint32_t *)((const uint8_t *)odt_td + a);
+}
+template <int K>
+DEVI uint32_t isbrep(uint32_t v, uint32_t lanec) {
+    const uint32_t a = __builtin_amdgcn_perm(v, lanec, 0x0c0c0000u | ((4u + K) << 8));
+    return ((const uint8_t *)odt_td)[a + 128u];
+}
+/* aes_decrypt<14> on the replicated table */
+DEVI void aes256_decrypt_rep(const uint32_t *dk, const uint32_t in[4], uint32_t out[4], uint32_t lanec) {
+    uint32_t s0 = in[0] ^ dk[0], s1 = in[1] ^ dk[1], s2 = in[2] ^ dk[2], s3 = in[3] ^ dk[3];
+#pragma unroll
+    for (int r = 1; r < 14; r++) {
+        uint32_t t0 = xor3(xor3(tdrep<3>(s0, lanec), ror32(tdrep<2>(s3, lanec), 8), ror32(tdrep<1>(s2, lanec), 16)),
+                           ror32(tdrep<0>(s1, lanec), 24), dk[4 * r + 0]);
+        uint32_t t1 = xor3(xor3(tdrep<3>(s1, lanec), ror32(tdrep<2>(s0, lanec), 8), ror32(tdrep<1>(s3, lanec), 16)),
+                           ror32(tdrep<0>(s2, lanec), 24), dk[4 * r + 1]);
+        uint32_t t2 = xor3(xor3(tdrep<3>(s2, lanec), ror32(tdrep<2>(s1, lanec), 8), ror32(tdrep<1>(s0, lanec), 16)),
+                           ror32(tdrep<0>(s3, lanec), 24), dk[4 * r + 2]);
+        uint32_t t3 = xor3(xor3(tdrep<3>(s3, lanec), ror32(tdrep<2>(s2, lanec), 8), ror32(tdrep<1>(s1, lanec), 16)),
+                           ror32(tdrep<0>(s0, lanec), 24), dk[4 * r + 3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint32_t *r = dk + 56;
+    out[0] = ((isbrep<3>(s0, lanec) << 24) | (isbrep<2>(s3, lanec) << 16) | (isbrep<1>(s2, lanec) << 8) | isbrep<0>(s1, lanec)) ^ r[0];
+    out[1] = ((isbrep<3>(s1, lanec) << 24) | (isbrep<2>(s0, lanec) << 16) | (isbrep<1>(s3, lanec) << 8) | isbrep<0>(s2, lanec)) ^ r[1];
+    out[2] = ((isbrep<3>(s2, lanec) << 24) | (isbrep<2>(s1, lanec) << 16) | (isbrep<1>(s0, lanec) << 8) | isbrep<0>(s3, lanec)) ^ r[2];
+    out[3] = ((isbrep<3>(s3, lanec) << 24) | (isbrep<2>(s2, lanec) << 16) | (isbrep<1>(s1, lanec) << 8) | isbrep<0>(s0, lanec)) ^ r[3];
+}
+
+#define ODT_CHECK_THREADS 512
+__global__ void __launch_bounds__(ODT_CHECK_THREADS, 4)   /* 2 workgroups (64 KiB table each) per CU */
 k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
             uint32_t stop_on_first, const uint32_t *keys) {
     __shared__ uint8_t cs[256];
     __shared__ aes_lds L;
     __shared__ uint32_t flag;
+    for (uint32_t k = threadIdx.x; k < 256u * ODT_TD_ROW / 4; k += blockDim.x) {
+        const uint32_t x = k >> 6, c = k & 63u;
+        odt_td[k] = c < 32u ? T->td0[x] : (uint32_t)T->inv_sbox[x];
+    }
     if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    const uint32_t lanec = (threadIdx.x & 31u) << 2;
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = g < e.count;
     uint32_t key[8];
@@ -314,7 +360,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     if (p.enc_len == 16u) {
         /* experimental 2-byte check (:98-101) */
         uint32_t ct[4] = {p.enc[0], p.enc[1], p.enc[2], p.enc[3]}, pt[4];
-        aes_decrypt<14>(L, dk, ct, pt);
+        aes256_decrypt_rep(dk, ct, pt, lanec);
         ok = ((pt[0] ^ p.iv[0]) >> 16) == 0x0300u;
     } else {
         /* SHA256 over the first min(len,1024) plaintext bytes == checksum (:104-123) */
@@ -328,7 +374,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
             for (int q = 0; q < 4; q++) {
                 const uint32_t *cp = p.enc + (b * 4u + q) * 4u;
                 uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
-                aes_decrypt<14>(L, dk, ct, pt);
+                aes256_decrypt_rep(dk, ct, pt, lanec);
 #pragma unroll
                 for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
             }
@@ -341,7 +387,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
             if ((uint32_t)q < (rem >> 4)) {
                 const uint32_t *cp = p.enc + (nfull * 4u + q) * 4u;
                 uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
-                aes_decrypt<14>(L, dk, ct, pt);
+                aes256_decrypt_rep(dk, ct, pt, lanec);
 #pragma unroll
                 for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
             } else {
@@ -693,7 +739,7 @@ hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_a
     if (e.mode == 0) hipLaunchKernelGGL(k_odt_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     else hipLaunchKernelGGL(k_odt_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     if (mid) (void)hipEventRecord(mid, s);
-    hipLaunchKernelGGL(k_odt_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
+    hipLaunchKernelGGL(k_odt_check, GRID(e.count, ODT_CHECK_THREADS), dim3(ODT_CHECK_THREADS), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
