@@ -224,3 +224,26 @@ def test_brute_force_module_end_to_end(dprf, streams):
     assert bf.init(streams["pdf_synth_r3_l128_abc"]["stream"], 3, None, devices=[0]) == (1, "abc")
     assert bf.init(streams["pdf_testdoc_r2"]["stream"], 2, None, devices=[0]) == (0, "default_password_allocation")
     assert bf.init(streams["office_testdoc"]["stream"], 0, ["x", "password", "y"], devices=[0]) == (1, "password")
+
+
+def test_multi_device_rounds_on_one_gpu(dprf, streams, monkeypatch):
+    """The multi-device code paths (one context and one host thread per device, contiguous slices of
+    each round) run here with two contexts on the same GPU: same answers as one device, and the lowest
+    hit wins when several slices hold hits."""
+    from dprf_amd import brute_force as bf
+    from dprf_amd import client as cl
+    from dprf_amd import payload as pl
+    monkeypatch.setattr(bf, "ROUND_PER_DEVICE", 4096)
+    s = streams["pdf_synth_r3_l128_abc"]["stream"]
+    for devs in ([0], [0, 0], [0, 0, 0]):
+        assert bf.init(s, 3, None, devices=devs) == (1, "abc")
+    e = streams["odt_testdoc_e"]["stream"]          # [a-z]^4 holds 10 hits of the 2-byte check
+    want = bf.init(e, 4, None, devices=[0])
+    assert bf.init(e, 4, None, devices=[0, 0, 0]) == want == (1, "bozc")
+    pws = ["zzzz", "yvgl", "aaaa", "bozc", "password"]
+    assert bf.init(e, 0, pws, devices=[0, 0]) == (1, "yvgl")
+    # GPU client verifier over two contexts: the lowest list index that verifies
+    ver = cl.GpuVerifier([0, 0])
+    blob, offs = pl._pack(pws)
+    assert ver(e, blob, offs) == (1, "yvgl")
+    ver.close()
