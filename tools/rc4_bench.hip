@@ -13,8 +13,8 @@
 #include <cstring>
 #include <vector>
 #include <algorithm>
+#include "../dprf_amd/csrc/dev_crypto.h"
 
-#define DEVI __device__ __forceinline__
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
@@ -274,6 +274,44 @@ static void occupancy(int blocks64, int wpb, uint32_t *dout) {
     CHECK(hipFree(drec));
 }
 
+
+/* co-scheduling probe: a pure-VALU kernel (52 MD5 compressions per lane, the R3/R4 key derivation's
+ * work) on a second stream while the LDS-bound RC4 kernel runs */
+__global__ void __launch_bounds__(256) k_md5x52(uint32_t *out) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    uint32_t h[4] = {mix(g), mix(g + 1u), mix(g + 2u), mix(g + 3u)};
+    for (int i = 0; i < 52; i++) {
+        uint32_t m[16] = {h[0], h[1], h[2], h[3], 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 128u, 0};
+        md5_iv(h);
+        md5_compress(h, m);
+    }
+    out[4 * g] = h[0] ^ h[1] ^ h[2] ^ h[3];
+}
+
+static void cosched(int blocks, uint32_t *dout, uint32_t *dout2) {
+    hipStream_t sa, sb;
+    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
+    const int mblocks = blocks / 4;   /* same number of lanes as the RC4 launch */
+    float t[3];
+    for (int mode = 0; mode < 3; mode++) {
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(a, 0));
+        for (int r = 0; r < 3; r++) {
+            if (mode != 1) hipLaunchKernelGGL(k_rc4<3>, dim3(blocks), dim3(64), 0, sa, dout);
+            if (mode != 0) hipLaunchKernelGGL(k_md5x52, dim3(mblocks), dim3(256), 0, sb, dout2);
+        }
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(b, 0));
+        CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&t[mode], a, b));
+    }
+    printf("co-scheduling: RC4 alone %.2f ms, MD5x52 alone %.2f ms, both on two streams %.2f ms (sum %.2f)\n",
+           t[0] / 3, t[1] / 3, t[2] / 3, (t[0] + t[1]) / 3);
+}
+
 static void cpu_ref(uint32_t g, uint32_t d[4]) {
     uint32_t h[4] = {mix(g), mix(g + 0x9e3779b9u), mix(g ^ 0x5bd1e995u), mix(g * 3u + 1u)};
     d[0] = 0x11111111u; d[1] = 0x22222222u; d[2] = 0x33333333u; d[3] = 0x44444444u;
@@ -329,5 +367,8 @@ int main(int argc, char **argv) {
                n / ms[v] / 1e3);
     occupancy(blocks, 1, dout);
     occupancy(blocks, 2, dout);
+    uint32_t *dout2;
+    CHECK(hipMalloc(&dout2, n * 16));
+    cosched(blocks, dout, dout2);
     return bad;
 }
