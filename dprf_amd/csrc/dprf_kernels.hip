@@ -410,44 +410,55 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
 }
 
 /* ================================================================== PDF R5 (one SHA-256) */
+/* One SHA-256 per candidate is ~2,300 cycles of a wave: with one candidate per thread, wave launch and
+ * the block prologue were a third of the kernel (2 Mi waves per 128 Mi-candidate launch).  Each thread
+ * now takes R5_PER candidates, 256 apart. */
+#define R5_PER 8
 template <int MODE>
 __global__ void __launch_bounds__(256)
 k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
     if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
-    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = g0 < e.count;
-    const uint32_t g = valid ? g0 : e.count - 1;
-    cand c;
-    get_candidate<MODE, false>(e, cs, g, c);
-    /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
-    uint32_t m[32];
+    const uint32_t base = blockIdx.x * (blockDim.x * R5_PER);
+#pragma unroll 1
+    for (uint32_t k = 0; k < R5_PER; k++) {
+        const uint32_t g0 = base + k * blockDim.x + threadIdx.x;
+        if (base + k * blockDim.x >= e.count) break;                 /* uniform */
+        const bool valid = g0 < e.count;
+        const uint32_t g = valid ? g0 : e.count - 1;
+        cand c;
+        get_candidate<MODE, false>(e, cs, g, c);
+        /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
+        uint32_t m[32];
 #pragma unroll
-    for (int j = 0; j < 32; j++) m[j] = j < DPRF_SLOT_WORDS ? (c.w[j] & le_keep_mask(j, c.len)) : 0u;
-    /* append the 8 validation-salt bytes (LE words p.u[8], p.u[9]) at byte offset len, then 0x80 */
-    const uint32_t sw[3] = {p.u[8], p.u[9], 0x80u};
-    const uint32_t q = c.len >> 2, r = (c.len & 3u) * 8u;
+        for (int j = 0; j < 32; j++) m[j] = j < DPRF_SLOT_WORDS ? (c.w[j] & le_keep_mask(j, c.len)) : 0u;
+        /* append the 8 validation-salt bytes (LE words p.u[8], p.u[9]) at byte offset len, then 0x80 */
+        const uint32_t sw[3] = {p.u[8], p.u[9], 0x80u};
+        const uint32_t q = c.len >> 2, r = (c.len & 3u) * 8u;
 #pragma unroll
-    for (int s = 0; s < 3; s++) {
-        const uint32_t lo = r ? (sw[s] << r) : sw[s];
-        const uint32_t hi = r ? (sw[s] >> (32u - r)) : 0u;
+        for (int s = 0; s < 3; s++) {
+            const uint32_t lo = r ? (sw[s] << r) : sw[s];
+            const uint32_t hi = r ? (sw[s] >> (32u - r)) : 0u;
 #pragma unroll
-        for (int j = 0; j < 32; j++) {
-            if ((uint32_t)j == q + s) m[j] |= lo;
-            if ((uint32_t)j == q + s + 1) m[j] |= hi;
+            for (int j = 0; j < 32; j++) {
+                if ((uint32_t)j == q + s) m[j] |= lo;
+                if ((uint32_t)j == q + s + 1) m[j] |= hi;
+            }
         }
+#pragma unroll
+        for (int j = 0; j < 32; j++) m[j] = bswap32(m[j]);
+        uint32_t hh[8];
+        sha256_msg2(m, c.len + 8u, hh);
+        bool ok = true;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) ok = ok && hh[kk] == p.u[kk];
+        if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
     }
-    /* 0x80 was appended as a byte after the salt: keep only its low byte contribution */
-#pragma unroll
-    for (int j = 0; j < 32; j++) m[j] = bswap32(m[j]);
-    uint32_t hh[8];
-    sha256_msg2(m, c.len + 8u, hh);
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 8; k++) ok = ok && hh[k] == p.u[k];
-    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
-    count_block(e, R);
+    if (threadIdx.x == 0) {
+        const uint32_t n = e.count - base < blockDim.x * R5_PER ? e.count - base : blockDim.x * R5_PER;
+        atomicAdd(&R->evaluated, (unsigned long long)n);
+    }
 }
 
 /* ================================================================== PDF R2..R4 (MD5 + RC4) */
@@ -744,8 +755,8 @@ hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_a
 }
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                          uint32_t stop, hipStream_t s) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_pdf_r5<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, cap, stop);
-    else hipLaunchKernelGGL(k_pdf_r5<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, cap, stop);
+    if (e.mode == 0) hipLaunchKernelGGL(k_pdf_r5<0>, GRID(e.count, 256 * R5_PER), dim3(256), 0, s, e, p, R, cap, stop);
+    else hipLaunchKernelGGL(k_pdf_r5<1>, GRID(e.count, 256 * R5_PER), dim3(256), 0, s, e, p, R, cap, stop);
     return hipGetLastError();
 }
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
