@@ -473,74 +473,62 @@ DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
 }
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
-DEVI uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-/* KSA with an NK-byte key held LE-packed in k[4], four steps per group.
+/* KSA with an NK-byte key held LE-packed in k[4].
  *
- * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions 4q..4q+3 are one LDS dword of this lane,
- * so group q reads that dword once and keeps the group's S[i] side of the swaps in a register:
- *  (A) the j chain runs from registers only: s_r (= S[4q+r] before step r) is byte r of the dword unless
- *      an earlier step of the group swapped into it (then it is that step's s);
- *  (B) each step reads S[j_r] and writes S[j_r] = s_r in program order, so every position outside the
- *      group is current in LDS (one wave's LDS operations complete in order);
- *  (C) the group's dword is rebuilt with two byte perms per step -- byte r <- S[j_r] (taken from the
- *      dword itself when j_r falls inside the group, whose LDS copy is stale), byte j_r&3 <- s_r when
- *      j_r is inside the group -- and stored once.
- * Per step that is one byte read + one byte write instead of two of each, and one dependent LDS round
- * trip per four steps.  Measured against the one-step-ahead schedule and a plain KSA on 4 Mi lanes
- * (tools/rc4_bench.hip, identical output): 390 / 370 / 334 M cand/s for 20 x (KSA + PRGA16); inside
- * k_pdf_r24 (with MD5 x52 and enumeration) +1 % over one-step-ahead.  At 16 KiB per wave only 9 waves
- * fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10), and with LDS-array ~45 % and VALU ~60 % busy the
- * loop is bound by the LDS round trips of 9 waves, not by either pipe. */
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions 4q..4q+3 are one LDS dword of this lane:
+ * group q reads that dword once, and s_r (= S[4q+r] before step r) is its byte r unless an earlier step
+ * of the group swapped into that position (S[j] = s with j = 4q+r; a compare-select per earlier step).
+ * So the j chain waits on LDS once per four steps.  Every step still reads S[j] and stores both sides of
+ * the swap in program order, so LDS is current for every position -- except that the S[i] = S[j] store
+ * is issued one step late (after the next step's S[j] read, which is repaired when it hits i), so the
+ * wave does not stall on its own read right after issuing it.
+ * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs): this
+ * schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a register and stored
+ * once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain 334 M.  At 16 KiB per
+ * wave only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     /* identity: the values are produced by an add chain kept opaque to the compiler, which would otherwise
-     * hoist 63 literal VGPRs out of the pass loop and halve occupancy */
+     * hoist 64 literal VGPRs out of the pass loop and halve occupancy */
     uint32_t iv = 0x03020100u;
 #pragma unroll
-    for (int w = 1; w < 64; w++) {
-        iv += 0x04040404u;
+    for (int w = 0; w < 64; w++) {
         asm volatile("" : "+v"(iv));
         *(uint32_t *)(S + (w << 8) + lanebase) = iv;
+        iv += 0x04040404u;
     }
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
     uint32_t j = 0;
-    uint32_t W = 0x03020100u;                   /* dword 0 is the identity: no store, no read */
+    uint32_t W = 0x03020100u;                   /* dword 0 is the identity */
+    uint32_t px = 0;                            /* S[i-1] value whose store is deferred */
 #pragma unroll
     for (int q = 0; q < 64; q++) {
         const uint32_t base = 4u * (uint32_t)q;
-        uint32_t s[4], m[4], x[4];
+        uint32_t s[4], m[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
+            const int i = 4 * q + r;
             uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
 #pragma unroll
             for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
             s[r] = v;
-            j = j + v + kb[(4 * q + r) % NK];
+            j = j + v + kb[i % NK];
             m[r] = j & 0xffu;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
             const uint32_t a = rc4_addr(m[r], lanebase);
-            x[r] = lds_ld8(S, a);
-            lds_st8(S, a, s[r]);
+            uint32_t x = lds_ld8(S, a);
+            if (i > 0) {
+                lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, px);
+                x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+            }
+            lds_st8(S, a, v);
+            px = x;
         }
-        uint32_t Wn = 0;
-        if (q < 63) Wn = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
-        uint32_t Wf = W;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const uint32_t v = umin32(m[r] - base, 4u);                 /* byte in the group; 4 = outside */
-            const uint32_t idr = 0x03020100u & ~(0xffu << (8 * r));
-            Wf = __builtin_amdgcn_perm(x[r], Wf, idr | (v << (8 * r)));    /* byte r <- S[j_r] */
-            const uint32_t sh = (v << 3) & 31u;                             /* v = 4: no-op selector */
-            Wf = __builtin_amdgcn_perm(s[r], Wf, 0x03020100u + ((4u - v) << sh)); /* byte v <- s_r */
-        }
-        *(uint32_t *)(S + (q << 8) + lanebase) = Wf;
-        W = Wn;
+        if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
     }
+    lds_st8(S, (63u << 8) + 3u + lanebase, px);
 }
 
 /* One-step-ahead KSA schedule, used for R2 (one KSA per candidate).  Step i issues its S[j_i] read and

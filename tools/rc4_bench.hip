@@ -5,6 +5,10 @@
  *   1  one-step-ahead prefetch with register repairs (the production kernel's schedule)
  *   2  one-step-ahead, repairs as VGPR masks (no v_cmp -> SGPR -> v_cndmask hazard)
  *   3  grouped: S[4q..4q+3] read as one dword, S[i] writes kept in a register and stored once per group
+ *   4  3 with the group loop rolled (instruction-fetch test)
+ *   5  dword-prefetched s values, both swap stores per step (no register bookkeeping of the S[i] side)
+ *   6  5 with the S[i] store deferred one step (the production schedule, dprf_kernels.hip rc4_ksa)
+ *   7  6 with the next dword read two steps earlier (repairs against the last two steps)
  * Usage: rc4_bench [blocks_per_launch] [reps] */
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -127,6 +131,104 @@ DEVI void ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             }
             Sq += 1024;
         }
+    } else if (V == 5) {
+        /* Dword-prefetched s values, per-step stores: group q reads S[4q..4q+3] as one dword; s_r is byte
+         * r unless an earlier step of the group swapped into it (S[j] = s with j = 4q+r).  Every step still
+         * reads S[j] and writes S[i] = S[j], S[j] = s_i in program order, so LDS stays current for every
+         * position and no in-group bookkeeping of the S[i] side is needed.  The j chain never waits on LDS
+         * except for the one dword per four steps. */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u;
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+#pragma unroll
+                for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+                s[r] = v;
+                j = j + v + kb[(4 * q + r) & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr(m[r], lanebase);
+                const uint32_t x = ld8(S, a);
+                st8(S, posaddr(4 * q + r, lanebase), x);
+                st8(S, a, v);
+            }
+            if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        }
+    } else if (V == 6) {
+        /* V5 with the S[i] = S[j] store deferred by one step, so the wave does not wait for the S[j] read
+         * right after issuing it: step r+1's read precedes step r's S[i] store and is repaired when
+         * j_{r+1} == i_r (it then must see x_r). */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u;
+        uint32_t pi = 0, px = 0;            /* deferred store: position, value */
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int i = 4 * q + r;
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+#pragma unroll
+                for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+                s[r] = v;
+                j = j + v + kb[i & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr(m[r], lanebase);
+                uint32_t x = ld8(S, a);
+                if (i > 0) {
+                    st8(S, posaddr(i - 1, lanebase), px);
+                    x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+                }
+                st8(S, a, v);
+                px = x;
+            }
+            if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        }
+        st8(S, posaddr(255, lanebase), px);
+        (void)pi;
+    } else if (V == 7) {
+        /* V6 with the next group's dword read issued after step 1 of the current group: steps 2 and 3 may
+         * still swap into the next group, so the next group's s values are also repaired against them. */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u, Wn = 0;
+        uint32_t px = 0;
+        uint32_t pm2 = 0xffffu, pm3 = 0xffffu, ps2 = 0, ps3 = 0;   /* previous group's steps 2, 3 */
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int i = 4 * q + r;
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+                if (q > 0) {
+                    v = (pm2 == base + (uint32_t)r) ? ps2 : v;
+                    v = (pm3 == base + (uint32_t)r) ? ps3 : v;
+                }
+#pragma unroll
+                for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+                s[r] = v;
+                j = j + v + kb[i & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr(m[r], lanebase);
+                uint32_t x = ld8(S, a);
+                if (i > 0) {
+                    st8(S, posaddr(i - 1, lanebase), px);
+                    x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+                }
+                st8(S, a, v);
+                px = x;
+                if (r == 1 && q < 63) Wn = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+            }
+            pm2 = m[2]; pm3 = m[3]; ps2 = s[2]; ps3 = s[3];
+            W = Wn;
+        }
+        st8(S, posaddr(255, lanebase), px);
     } else if (V == 3) {
         /* Grouped.  Group q covers positions 4q..4q+3 (one LDS dword of this lane).  Phase A (register only)
          * runs the j chain: s_r = value at position 4q+r before step r = the dword's byte r unless an
@@ -352,7 +454,7 @@ int main(int argc, char **argv) {
     uint32_t *dout;
     CHECK(hipMalloc(&dout, n * 16));
     std::vector<uint32_t> ref(n * 4), got(n * 4);
-    double ms[5];
+    double ms[8];
     ms[0] = run<0>(blocks, reps, dout, ref);
     for (size_t g = 0; g < n; g += 9973) {
         uint32_t d[4];
@@ -361,8 +463,8 @@ int main(int argc, char **argv) {
     }
     int bad = 0;
 #define VAR(V) ms[V] = run<V>(blocks, reps, dout, got); if (got != ref) { printf("variant %d MISMATCH\n", V); bad = 1; }
-    VAR(1) VAR(2) VAR(3) VAR(4)
-    for (int v = 0; v < 5; v++)
+    VAR(1) VAR(2) VAR(3) VAR(4) VAR(5) VAR(6) VAR(7)
+    for (int v = 0; v < 8; v++)
         printf("variant %d: %.3f ms / launch of %zu lanes -> %.1f M cand/s (20 x KSA+PRGA16)\n", v, ms[v], n,
                n / ms[v] / 1e3);
     occupancy(blocks, 1, dout);
