@@ -474,6 +474,33 @@ DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
 
+/* S = identity for every lane of the wave: dword w of lane l is at S + 256 w + 4 l, exactly the address
+ * ds_write_addtid_b32 forms from M0 + offset + 4 * lane, so the 64 stores carry no address VGPR.  One asm
+ * block: the values come from an add chain the compiler cannot hoist out of the pass loop as 64 literal
+ * VGPRs; M0 is reserved to the compiler, so the block restores it. */
+DEVI void rc4_identity(uint8_t *S) {
+    const uint32_t base = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)S;
+    uint32_t t, m0save;
+#define RC4_ID_W(o) "ds_write_addtid_b32 %0 offset:" #o "\n\tv_add_u32 %0, 0x4040404, %0\n\t"
+    asm volatile(
+        "s_mov_b32 %1, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "v_mov_b32 %0, 0x3020100\n\t"
+        RC4_ID_W(0) RC4_ID_W(256) RC4_ID_W(512) RC4_ID_W(768) RC4_ID_W(1024) RC4_ID_W(1280) RC4_ID_W(1536) RC4_ID_W(1792)
+        RC4_ID_W(2048) RC4_ID_W(2304) RC4_ID_W(2560) RC4_ID_W(2816) RC4_ID_W(3072) RC4_ID_W(3328) RC4_ID_W(3584) RC4_ID_W(3840)
+        RC4_ID_W(4096) RC4_ID_W(4352) RC4_ID_W(4608) RC4_ID_W(4864) RC4_ID_W(5120) RC4_ID_W(5376) RC4_ID_W(5632) RC4_ID_W(5888)
+        RC4_ID_W(6144) RC4_ID_W(6400) RC4_ID_W(6656) RC4_ID_W(6912) RC4_ID_W(7168) RC4_ID_W(7424) RC4_ID_W(7680) RC4_ID_W(7936)
+        RC4_ID_W(8192) RC4_ID_W(8448) RC4_ID_W(8704) RC4_ID_W(8960) RC4_ID_W(9216) RC4_ID_W(9472) RC4_ID_W(9728) RC4_ID_W(9984)
+        RC4_ID_W(10240) RC4_ID_W(10496) RC4_ID_W(10752) RC4_ID_W(11008) RC4_ID_W(11264) RC4_ID_W(11520) RC4_ID_W(11776) RC4_ID_W(12032)
+        RC4_ID_W(12288) RC4_ID_W(12544) RC4_ID_W(12800) RC4_ID_W(13056) RC4_ID_W(13312) RC4_ID_W(13568) RC4_ID_W(13824) RC4_ID_W(14080)
+        RC4_ID_W(14336) RC4_ID_W(14592) RC4_ID_W(14848) RC4_ID_W(15104) RC4_ID_W(15360) RC4_ID_W(15616) RC4_ID_W(15872) RC4_ID_W(16128)
+        "s_mov_b32 m0, %1"
+        : "=&v"(t), "=&s"(m0save)
+        : "s"(base)
+        : "memory");
+#undef RC4_ID_W
+}
+
 /* KSA with an NK-byte key held LE-packed in k[4].
  *
  * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions 4q..4q+3 are one LDS dword of this lane:
@@ -489,15 +516,7 @@ DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v;
  * wave only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
-    /* identity: the values are produced by an add chain kept opaque to the compiler, which would otherwise
-     * hoist 64 literal VGPRs out of the pass loop and halve occupancy */
-    uint32_t iv = 0x03020100u;
-#pragma unroll
-    for (int w = 0; w < 64; w++) {
-        asm volatile("" : "+v"(iv));
-        *(uint32_t *)(S + (w << 8) + lanebase) = iv;
-        iv += 0x04040404u;
-    }
+    rc4_identity(S);
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
