@@ -471,6 +471,15 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
 DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
     return ((__builtin_amdgcn_ubfe(j, 2, 6)) << 8) | (j & 3u) | lanebase;
 }
+/* rc4_addr in two half-rate instructions: (j & 3) | lanebase, then byte 1 <- (j & 0xff) >> 2 by an SDWA shift
+ * that keeps the other bytes (lanebase < 256).  tools/rc4_bench.hip variant 9: +3.6% on the R3/R4 KSA; the
+ * R2 kernel (one KSA per candidate, ahead schedule) measured 6% slower with it, so it keeps rc4_addr. */
+DEVI uint32_t rc4_addr_sdwa(uint32_t j, uint32_t lanebase) {
+    uint32_t t = (j & 3u) | lanebase;
+    asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+        : "+v"(t) : "v"(j));
+    return t;
+}
 DEVI uint32_t lds_ld8(const uint8_t *base, uint32_t a) { return base[a]; }
 DEVI void lds_st8(uint8_t *base, uint32_t a, uint32_t v) { base[a] = (uint8_t)v; }
 
@@ -536,7 +545,7 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             s[r] = v;
             j = j + v + kb[i % NK];
             m[r] = j & 0xffu;
-            const uint32_t a = rc4_addr(m[r], lanebase);
+            const uint32_t a = rc4_addr_sdwa(m[r], lanebase);
             uint32_t x = lds_ld8(S, a);
             if (i > 0) {
                 lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, px);

@@ -9,6 +9,8 @@
  *   5  dword-prefetched s values, both swap stores per step (no register bookkeeping of the S[i] side)
  *   6  5 with the S[i] store deferred one step (the production schedule, dprf_kernels.hip rc4_ksa)
  *   7  6 with the next dword read two steps earlier (repairs against the last two steps)
+ *   9  6 with the S[j] address in two instructions (SDWA byte-1 shift)
+ *   8  6 with the S[i] repair applied lazily at the deferred store (first use of a read one step later)
  * Usage: rc4_bench [blocks_per_launch] [reps] */
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -23,6 +25,12 @@
 
 DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
     return ((__builtin_amdgcn_ubfe(j, 2, 6)) << 8) | (j & 3u) | lanebase;
+}
+DEVI uint32_t rc4_addr_sdwa(uint32_t j, uint32_t lanebase) {
+    uint32_t t = (j & 3u) | lanebase;
+    asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+        : "+v"(t) : "v"(j));
+    return t;
 }
 DEVI uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 DEVI uint32_t ld8(const uint8_t *b, uint32_t a) { return b[a]; }
@@ -191,6 +199,73 @@ DEVI void ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
         }
         st8(S, posaddr(255, lanebase), px);
         (void)pi;
+    } else if (V == 8) {
+        /* V6 with the repair of x_i (j_i == i-1 -> the still-pending S[i-1]) applied lazily, right before x_i
+         * is stored one step later: the wave's first use of a read is then after the next step's read, so the
+         * wait covers a step of VALU work.  The asm statement pins that use after the read. */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u;
+        uint32_t praw = 0, pflag = 0, pxf = 0;   /* x_{i-1} raw, (j_{i-1} == i-2), x_{i-2} final */
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int i = 4 * q + r;
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+#pragma unroll
+                for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+                s[r] = v;
+                j = j + v + kb[i & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr(m[r], lanebase);
+                const uint32_t x = ld8(S, a);
+                if (i > 0) {
+                    asm volatile("" : "+v"(praw) :: "memory");
+                    const uint32_t xf = pflag ? pxf : praw;        /* x_{i-1} final */
+                    st8(S, posaddr(i - 1, lanebase), xf);
+                    pxf = xf;
+                    pflag = m[r] == (uint32_t)(i - 1);
+                }
+                st8(S, a, v);
+                praw = x;
+            }
+            if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        }
+        asm volatile("" : "+v"(praw) :: "memory");
+        st8(S, posaddr(255, lanebase), pflag ? pxf : praw);
+    } else if (V == 9) {
+        /* V6 with the S[j] address built in two instructions: (j & 3) | lanebase, then byte 1 <- (j & 0xff) >> 2
+         * by an SDWA shift that preserves the other bytes (rc4_addr: three instructions, two half-rate). */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u;
+        uint32_t px = 0;
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int i = 4 * q + r;
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+#pragma unroll
+                for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
+                s[r] = v;
+                j = j + v + kb[i & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr_sdwa(j, lanebase);
+                uint32_t x = ld8(S, a);
+                if (i > 0) {
+                    st8(S, posaddr(i - 1, lanebase), px);
+                    x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+                }
+                st8(S, a, v);
+                px = x;
+            }
+            if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        }
+        st8(S, posaddr(255, lanebase), px);
     } else if (V == 7) {
         /* V6 with the next group's dword read issued after step 1 of the current group: steps 2 and 3 may
          * still swap into the next group, so the next group's s values are also repaired against them. */
@@ -454,7 +529,7 @@ int main(int argc, char **argv) {
     uint32_t *dout;
     CHECK(hipMalloc(&dout, n * 16));
     std::vector<uint32_t> ref(n * 4), got(n * 4);
-    double ms[8];
+    double ms[10];
     ms[0] = run<0>(blocks, reps, dout, ref);
     for (size_t g = 0; g < n; g += 9973) {
         uint32_t d[4];
@@ -463,8 +538,8 @@ int main(int argc, char **argv) {
     }
     int bad = 0;
 #define VAR(V) ms[V] = run<V>(blocks, reps, dout, got); if (got != ref) { printf("variant %d MISMATCH\n", V); bad = 1; }
-    VAR(1) VAR(2) VAR(3) VAR(4) VAR(5) VAR(6) VAR(7)
-    for (int v = 0; v < 8; v++)
+    VAR(1) VAR(2) VAR(3) VAR(4) VAR(5) VAR(6) VAR(7) VAR(8) VAR(9)
+    for (int v = 0; v < 10; v++)
         printf("variant %d: %.3f ms / launch of %zu lanes -> %.1f M cand/s (20 x KSA+PRGA16)\n", v, ms[v], n,
                n / ms[v] / 1e3);
     occupancy(blocks, 1, dout);

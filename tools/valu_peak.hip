@@ -78,6 +78,15 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
                 asm volatile("v_add_co_u32_e64 %0, %2, %0, %3\n\tv_addc_co_u32_e64 %1, %2, %1, %4, %2"
                              : "+v"(x[c]), "+v"(x[(c + 1) & (CHAINS - 1)]), "=&s"(cc) : "v"(y), "v"(z));
             }
+            if (OP == 45) asm volatile("v_cmp_eq_u32_sdwa vcc, %0, %1 src0_sel:BYTE_0 src1_sel:DWORD" : : "v"(x[c]), "v"(y) : "vcc");
+            if (OP == 46) { unsigned long long msk; asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(msk) : "v"(x[c]), "v"(y)); x[c] += (unsigned)msk; }
+            if (OP == 47) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "s"((unsigned long long)z));
+            if (OP == 48) { /* select through a VGPR mask: bfi(mask, a, b) */
+                asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(x[c]) : "v"(y), "v"(z)); }
+            if (OP == 49) asm volatile("v_min_u32_e32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 50) asm volatile("v_cmp_eq_u32_sdwa vcc, %0, %1 src0_sel:BYTE_0 src1_sel:DWORD\n\ts_nop 1\n\tv_cndmask_b32_e32 %0, %0, %2, vcc" : "+v"(x[c]) : "v"(y), "v"(z) : "vcc");
+            if (OP == 51) asm volatile("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0" : "+v"(x[c]) : "v"(y));
+            if (OP == 52) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "+v"(x[c]) : "v"(y));
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -118,6 +127,19 @@ double run(const char *name, int blocks, int per_iter) {
 int main() {
     const int blocks = 32768;
     run<3>("v_xor_b32", blocks, 1);
+    run<31>("v_cndmask vcc", blocks, 1);
+    run<47>("v_cndmask e64 s", blocks, 1);
+    run<38>("v_cmp_eq e32", blocks, 1);
+    run<45>("v_cmp_eq sdwa", blocks, 1);
+    run<46>("v_cmp_eq e64+add", blocks, 2);
+    run<36>("cmp+cndmask vcc", blocks, 2);
+    run<37>("cmp+cndmask e64", blocks, 2);
+    run<50>("cmp_sdwa+nop+cnd", blocks, 2);
+    run<39>("xor-mask select", blocks, 6);
+    run<48>("v_bfi_b32", blocks, 1);
+    run<51>("lshr sdwa byte1", blocks, 1);
+    run<52>("add sdwa byte0", blocks, 1);
+    run<49>("v_min_u32", blocks, 1);
     run<40>("add_co+addc (vcc) pair", blocks, 2);
     run<44>("add_co+addc e64 pair", blocks, 2);
     run<41>("v_lshl_add_u64", blocks, 1);
