@@ -322,7 +322,10 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
  * Pattern areas: slots [0, te_slots) live in the free upper halves of the Te0 rows in groups of 32
  * (column 128 + 4*(slot%32)), the rest in the dynamic area in groups of 64 (column 4*(slot%64)); rows are
  * 256 bytes apart in both, so r6_read16 and friends see one layout. */
+#ifndef R6_LANES
 #define R6_LANES 768
+#endif
+#define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
 #define R6_MAX_SLOTS 1280
 #define R6_CLASSES 7                    /* 6 live classes + "no candidate" */
 #define R6_IDLE 0xffffffffu
@@ -412,9 +415,9 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         __syncthreads();
         R6T_MARK(t_bar)
         /* 1. family of each slot this thread looks after; rank within its class by an LDS atomic */
-        uint32_t mycls[2], myrank[2], myh[2];
+        uint32_t mycls[R6_SLOTS_PER_THREAD], myrank[R6_SLOTS_PER_THREAD], myh[R6_SLOTS_PER_THREAD];
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < R6_SLOTS_PER_THREAD; q++) {
             const uint32_t sl = tid + (uint32_t)q * nthr;
             mycls[q] = R6_CLASSES - 1; myh[q] = 0; myrank[q] = 0;
             if (sl < nslots) {
@@ -431,7 +434,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         R6T_MARK(t_bar)
         if (sh->hist[R6_CLASSES - 1] == nslots) break;             /* no slot has a candidate: uniform exit */
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < R6_SLOTS_PER_THREAD; q++) {
             const uint32_t sl = tid + (uint32_t)q * nthr;
             if (sl < nslots) {
                 uint32_t pos = myrank[q];

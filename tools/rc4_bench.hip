@@ -9,6 +9,7 @@
  *   5  dword-prefetched s values, both swap stores per step (no register bookkeeping of the S[i] side)
  *   6  5 with the S[i] store deferred one step (the production schedule, dprf_kernels.hip rc4_ksa)
  *   7  6 with the next dword read two steps earlier (repairs against the last two steps)
+ *  10-12 timing probes (not RC4): 9 without repairs / also without the group dword read / px repair only
  *   9  6 with the S[j] address in two instructions (SDWA byte-1 shift)
  *   8  6 with the S[i] repair applied lazily at the deferred store (first use of a read one step later)
  * Usage: rc4_bench [blocks_per_launch] [reps] */
@@ -264,6 +265,37 @@ DEVI void ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
                 px = x;
             }
             if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        }
+        st8(S, posaddr(255, lanebase), px);
+    } else if (V == 10 || V == 11 || V == 12) {
+        /* timing probes, NOT RC4 (results differ): 10 = variant 9 without any repair; 11 = 10 without the
+         * per-group dword re-read (no LDS wait on the j chain); 12 = 9 with the px repair but no s repairs */
+        uint32_t j = 0;
+        uint32_t W = 0x03020100u;
+        uint32_t px = 0;
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const uint32_t base = 4u * (uint32_t)q;
+            uint32_t s[4], m[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int i = 4 * q + r;
+                uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+                s[r] = v;
+                j = j + v + kb[i & 15];
+                m[r] = j & 0xffu;
+                const uint32_t a = rc4_addr_sdwa(j, lanebase);
+                uint32_t x = ld8(S, a);
+                if (i > 0) {
+                    st8(S, posaddr(i - 1, lanebase), px);
+                    if (V == 12) x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+                }
+                st8(S, a, v);
+                px = x;
+            }
+            (void)base; (void)s;
+            if (V != 11) { if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase); }
+            else W = W * 0x01010101u + px;
         }
         st8(S, posaddr(255, lanebase), px);
     } else if (V == 7) {
@@ -529,7 +561,7 @@ int main(int argc, char **argv) {
     uint32_t *dout;
     CHECK(hipMalloc(&dout, n * 16));
     std::vector<uint32_t> ref(n * 4), got(n * 4);
-    double ms[10];
+    double ms[13];
     ms[0] = run<0>(blocks, reps, dout, ref);
     for (size_t g = 0; g < n; g += 9973) {
         uint32_t d[4];
@@ -539,7 +571,8 @@ int main(int argc, char **argv) {
     int bad = 0;
 #define VAR(V) ms[V] = run<V>(blocks, reps, dout, got); if (got != ref) { printf("variant %d MISMATCH\n", V); bad = 1; }
     VAR(1) VAR(2) VAR(3) VAR(4) VAR(5) VAR(6) VAR(7) VAR(8) VAR(9)
-    for (int v = 0; v < 10; v++)
+    ms[10] = run<10>(blocks, reps, dout, got); ms[11] = run<11>(blocks, reps, dout, got); ms[12] = run<12>(blocks, reps, dout, got);
+    for (int v = 0; v < 13; v++)
         printf("variant %d: %.3f ms / launch of %zu lanes -> %.1f M cand/s (20 x KSA+PRGA16)\n", v, ms[v], n,
                n / ms[v] / 1e3);
     occupancy(blocks, 1, dout);
