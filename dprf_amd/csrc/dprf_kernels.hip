@@ -645,25 +645,13 @@ DEVI void rc4_prga<2>(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
     d[0] ^= k1 | (k2 << 8);
 }
 
+/* RC4 key of candidate g: MD5(pw[:32] || PAD[0:32-len] || O || LE32(P) || ID [|| FFFFFFFF]) (pdf...c:136-139,
+ * :352-402), then 50 x MD5(h[0:n]) for R >= 3 (:150-155).  Reads the charset and PAD from the LDS overlay. */
 template <int MODE, int R, int NK>
-__global__ void __launch_bounds__(64, 3)   /* <= 170 VGPRs: 3 waves/SIMD >= the 2.5 the LDS allows */
-k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
-    /* overlaid on the S-box area; all reads of these happen before the first KSA writes it (one wave per
-     * workgroup, LDS operations of a wave complete in order) */
-    uint8_t *cs = S;                                      /* charset, 256 B */
-    uint32_t *flag = (uint32_t *)(S + 256);
-    uint32_t *padw = (uint32_t *)(S + 320);               /* PAD || PAD for the runtime-offset padding */
-    if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
-    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag)) return;
-    const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = g0 < e.count;
-    const uint32_t g = valid ? g0 : e.count - 1;
+DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, const uint32_t *padw,
+                  uint32_t g, uint32_t h[4]) {
     cand c;
     get_candidate<MODE, false>(e, cs, g, c);
-    const uint32_t lanebase = (threadIdx.x & 63u) << 2;
-
-    /* padded password pw[:32] || PAD[0:32-len] (pdf...c:136-139), LE words */
     const uint32_t len = c.len > 32u ? 32u : c.len;
     uint32_t pw[8];
 #pragma unroll
@@ -676,8 +664,6 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
         }
         pw[j] = v;
     }
-    /* initial hash MD5(padded || O || LE32(P) || ID [|| FFFFFFFF]) (:352-402) */
-    uint32_t h[4];
     {
         uint32_t m[16];
 #pragma unroll
@@ -691,7 +677,6 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
         }
     }
     if (R >= 3) {
-        /* 50 x MD5(h[0:n]) (:150-155) */
         for (int i = 0; i < 50; i++) {
             uint32_t m[16];
             if (NK == 16) {
@@ -709,43 +694,87 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             md5_compress(h, m);
         }
     }
+}
+
+/* Candidates per lane: R2's single KSA is short enough that wave launch and the block prologue were a
+ * visible part of the kernel, so an R2 lane takes R24_PER_R2 candidates 64 apart; their keys are derived
+ * first, while the charset is still in the LDS overlay the KSA then overwrites. */
+#ifndef R24_PER_R2
+#define R24_PER_R2 4
+#endif
+template <int R> struct r24_per { static constexpr int v = R == 2 ? R24_PER_R2 : 1; };
+
+template <int MODE, int R, int NK>
+__global__ void __launch_bounds__(64, 3)   /* <= 170 VGPRs: 3 waves/SIMD >= the 2.5 the LDS allows */
+k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
+    constexpr int PER = r24_per<R>::v;
+    __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
+    /* overlaid on the S-box area; all reads of these happen before the first KSA writes it (one wave per
+     * workgroup, LDS operations of a wave complete in order) */
+    uint8_t *cs = S;                                      /* charset, 256 B */
+    uint32_t *flag = (uint32_t *)(S + 256);
+    uint32_t *padw = (uint32_t *)(S + 320);               /* PAD || PAD for the runtime-offset padding */
+    if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
+    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag)) return;
+    const uint32_t base = blockIdx.x * (64u * PER);
+    const uint32_t lanebase = (threadIdx.x & 63u) << 2;
+    uint32_t hk[PER][4];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t g0 = base + 64u * k + threadIdx.x;
+        r24_key<MODE, R, NK>(e, p, cs, padw, g0 < e.count ? g0 : e.count - 1, hk[k]);
+    }
     /* R3/R4 early reject: every pass first produces only 2 keystream bytes and the candidate survives iff
      * c19[0:2] equals U[0:2] (byte b of each pass is data[b] ^ keystream[b]).  A wave in which some lane
      * survives (2^-16 per lane) redoes its candidates with the full keystream and the reference's complete
      * 16-byte compare (:184-189). */
     uint8_t *Sw = S;   /* one wave per block: the whole array is this wave's */
-    bool ok = false;
-    if (R == 2) {
-        /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189) */
-        uint32_t d[8];
+#pragma unroll 1
+    for (uint32_t k = 0; k < (uint32_t)PER; k++) {
+        if (base + 64u * k >= e.count) break;                                       /* uniform */
+        const uint32_t g = base + 64u * k + threadIdx.x;
+        const bool valid = g < e.count;
+        const uint32_t h[4] = {hk[0][0], hk[0][1], hk[0][2], hk[0][3]};
 #pragma unroll
-        for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-        rc4_ksa_ahead<5>(Sw, lanebase, h);
-        rc4_prga<32>(Sw, lanebase, d);
-        ok = true;
+        for (int kk = 0; kk + 1 < PER; kk++)                       /* static rotation, no indexed registers */
 #pragma unroll
-        for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
-    } else {
-        /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
-        for (uint32_t full = 0; full < 2u; full++) {
-            uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
-            for (uint32_t x = 0; x < 20u; x++) {
-                const uint32_t xx = x * 0x01010101u;
-                uint32_t k[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-                rc4_ksa<NK>(Sw, lanebase, k);
-                if (full) rc4_prga<16>(Sw, lanebase, d);
-                else rc4_prga<2>(Sw, lanebase, d);
-            }
-            if (full) {
-                ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
-            } else {
-                const bool pre = ((d[0] ^ p.u[0]) & 0xffffu) == 0u;
-                if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
+            for (int q = 0; q < 4; q++) hk[kk][q] = hk[kk + 1][q];
+        bool ok = false;
+        if (R == 2) {
+            /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189) */
+            uint32_t d[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) d[j] = p.pad[j];
+            rc4_ksa_ahead<5>(Sw, lanebase, h);
+            rc4_prga<32>(Sw, lanebase, d);
+            ok = true;
+#pragma unroll
+            for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
+        } else {
+            /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
+            for (uint32_t full = 0; full < 2u; full++) {
+                uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
+                for (uint32_t x = 0; x < 20u; x++) {
+                    const uint32_t xx = x * 0x01010101u;
+                    uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
+                    rc4_ksa<NK>(Sw, lanebase, kx);
+                    if (full) rc4_prga<16>(Sw, lanebase, d);
+                    else rc4_prga<2>(Sw, lanebase, d);
+                }
+                if (full) {
+                    ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
+                } else {
+                    const bool pre = ((d[0] ^ p.u[0]) & 0xffffu) == 0u;
+                    if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
+                }
             }
         }
+        if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
     }
-    if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
-    count_block(e, R_);
+    if (threadIdx.x == 0) {
+        const uint32_t n = e.count - base < 64u * PER ? e.count - base : 64u * PER;
+        atomicAdd(&R_->evaluated, (unsigned long long)n);
+    }
 }
 
 /* ------------------------------------------------------------------ launchers */
@@ -777,7 +806,7 @@ hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_resu
 }
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                           uint32_t stop, hipStream_t s) {
-#define L24(M, RR, NK) hipLaunchKernelGGL((k_pdf_r24<M, RR, NK>), GRID(e.count, 64), dim3(64), 0, s, e, p, R, cap, stop)
+#define L24(M, RR, NK) hipLaunchKernelGGL((k_pdf_r24<M, RR, NK>), GRID(e.count, 64 * r24_per<RR>::v), dim3(64), 0, s, e, p, R, cap, stop)
     if (p.R == 2) { if (e.mode == 0) L24(0, 2, 5); else L24(1, 2, 5); }
     else if (p.n == 16) { if (e.mode == 0) L24(0, 3, 16); else L24(1, 3, 16); }
     else { if (e.mode == 0) L24(0, 3, 5); else L24(1, 3, 5); }

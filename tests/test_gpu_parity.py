@@ -209,6 +209,31 @@ def test_range_split_consistency(dprf, streams):
     assert s == total and pieces == whole and len(whole) >= 1
 
 
+def test_r2_ragged_ranges(dprf, streams):
+    """R2 lanes take several candidates each (k_pdf_r24, R24_PER_R2): counts that are not a multiple of a
+    block's candidates, and a start that is not block-aligned, give the same hits and counted candidates."""
+    c = ctx_for(dprf, streams, "pdf_synth_r2_key")
+    pw = streams["pdf_synth_r2_key"]["password"]
+    idx = 0
+    for ch in pw:
+        idx = idx * 26 + LOWER.index(ch)
+    total = 26 ** len(pw)
+    whole, n, st = c.search_range(LOWER, len(pw), 0, total)
+    assert idx in whole and st["candidates"] == total
+    pieces, s = [], 0
+    for step in [1, 63, 65, 255, 257, 1000, 4097, total]:
+        k = min(step, total - s)
+        if k <= 0:
+            break
+        h, _, st = c.search_range(LOWER, len(pw), s, k)
+        assert st["candidates"] == k
+        pieces += h
+        s += k
+    assert s == total and pieces == whole
+    hits, _, _ = c.search_range(LOWER, len(pw), idx - 5, 11, stop_on_first=True, cap=1)
+    assert hits == [idx]
+
+
 def test_list_mode_equals_range_mode(dprf, streams):
     from dprf_amd import brute_force as bf
     c = ctx_for(dprf, streams, "pdf_synth_r5_alnum")
