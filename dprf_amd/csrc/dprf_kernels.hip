@@ -421,6 +421,29 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
     __shared__ uint32_t flag;
     if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
     const uint32_t base = blockIdx.x * (blockDim.x * R5_PER);
+    /* Range mode: every candidate has length pwlen <= DPRF_MAX_RANGE_LEN, so the message is one block and
+     * its tail -- salt8 || 0x80 at byte pwlen, the bit length in word 15 -- is the same for the whole
+     * launch: 16 uniform BE words built once (SGPRs), OR-ed onto the candidate's BE words. */
+    uint32_t tail[16];
+    if (MODE == 0) {
+        const uint32_t len = e.pwlen, q = len >> 2, r = (len & 3u) * 8u;
+        const uint32_t sw[3] = {p.u[8], p.u[9], 0x80u};
+#pragma unroll
+        for (int j = 0; j < 16; j++) tail[j] = 0u;
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const uint32_t lo = r ? (sw[s] << r) : sw[s];
+            const uint32_t hi = r ? (sw[s] >> (32u - r)) : 0u;
+#pragma unroll
+            for (int j = 0; j < 15; j++) {
+                if ((uint32_t)j == q + s) tail[j] |= lo;
+                if ((uint32_t)j == q + s + 1) tail[j] |= hi;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 15; j++) tail[j] = bswap32(tail[j]);
+        tail[15] = (len + 8u) * 8u;
+    }
 #pragma unroll 1
     for (uint32_t k = 0; k < R5_PER; k++) {
         const uint32_t g0 = base + k * blockDim.x + threadIdx.x;
@@ -429,6 +452,20 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
         const uint32_t g = valid ? g0 : e.count - 1;
         cand c;
         get_candidate<MODE, false>(e, cs, g, c);
+        if (MODE == 0) {
+            /* range_candidate leaves the bytes past pwlen zero */
+            uint32_t b[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) b[j] = (j < DPRF_MAX_RANGE_LEN / 4 ? bswap32(c.w[j]) : 0u) | tail[j];
+            uint32_t hh[8];
+            sha256_iv(hh);
+            sha256_compress(hh, b);
+            bool ok = true;
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) ok = ok && hh[kk] == p.u[kk];
+            if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+            continue;
+        }
         /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
         uint32_t m[32];
 #pragma unroll
