@@ -686,20 +686,26 @@ DEVI void rc4_prga<2>(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
  * :352-402), then 50 x MD5(h[0:n]) for R >= 3 (:150-155).  Reads the charset and PAD from the LDS overlay. */
 template <int MODE, int R, int NK>
 DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, const uint32_t *padw,
-                  uint32_t g, uint32_t h[4]) {
+                  const uint32_t padtail[8], uint32_t g, uint32_t h[4]) {
     cand c;
     get_candidate<MODE, false>(e, cs, g, c);
     const uint32_t len = c.len > 32u ? 32u : c.len;
     uint32_t pw[8];
+    if (MODE == 0) {
+        /* range mode: pwlen <= 32 and the bytes past it are zero; PAD at offset pwlen is launch-uniform */
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        uint32_t v = c.w[j] & le_keep_mask(j, len);
+        for (int j = 0; j < 8; j++) pw[j] = c.w[j] | padtail[j];
+    } else {
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint32_t k = 4u * j + b;
-            if (k >= len) v |= (uint32_t)((const uint8_t *)padw)[k - len] << (8 * b);
+        for (int j = 0; j < 8; j++) {
+            uint32_t v = c.w[j] & le_keep_mask(j, len);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint32_t k = 4u * j + b;
+                if (k >= len) v |= (uint32_t)((const uint8_t *)padw)[k - len] << (8 * b);
+            }
+            pw[j] = v;
         }
-        pw[j] = v;
     }
     {
         uint32_t m[16];
@@ -755,11 +761,28 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag)) return;
     const uint32_t base = blockIdx.x * (64u * PER);
     const uint32_t lanebase = (threadIdx.x & 63u) << 2;
+    /* range mode: PAD[0:32-pwlen] placed at byte pwlen (pdf...c:136-139), 8 LE words, launch-uniform */
+    uint32_t padtail[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) padtail[j] = 0u;
+    if (MODE == 0) {
+        const uint32_t q = e.pwlen >> 2, r = (e.pwlen & 3u) * 8u;
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const uint32_t lo = r ? (p.pad[t] << r) : p.pad[t];
+            const uint32_t hi = r ? (p.pad[t] >> (32u - r)) : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if ((uint32_t)j == q + t) padtail[j] |= lo;
+                if ((uint32_t)j == q + t + 1) padtail[j] |= hi;
+            }
+        }
+    }
     uint32_t hk[PER][4];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const uint32_t g0 = base + 64u * k + threadIdx.x;
-        r24_key<MODE, R, NK>(e, p, cs, padw, g0 < e.count ? g0 : e.count - 1, hk[k]);
+        r24_key<MODE, R, NK>(e, p, cs, padw, padtail, g0 < e.count ? g0 : e.count - 1, hk[k]);
     }
     /* R3/R4 early reject: every pass first produces only 2 keystream bytes and the candidate survives iff
      * c19[0:2] equals U[0:2] (byte b of each pass is data[b] ^ keystream[b]).  A wave in which some lane
