@@ -299,6 +299,8 @@ def main():
             side[name] = {"value": sc * world / sdt, "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
                           "avg_launch_ms": skm / max(1, sl),
                           "valu_floor_frac": (sc / max(1, sl)) * work.per_candidate(skey) / (skm / max(1, sl) / 1e3) / peak}
+            if work.BOUND.get(skey) == "lds":
+                side[name]["lds_cycle_frac"] = work.lds_frac(skey, (sc / max(1, sl)) / (skm / max(1, sl) / 1e3))
             sctx.close()
 
     if rank == 0:
@@ -327,7 +329,8 @@ def main():
                          "floor_instr_per_candidate": floor,
                          "all_kernels_avg_ms": kern_ms / max(1, launches),
                          "all_kernels_frac": cands * work.per_candidate(wkey) / (kern_ms / 1e3) / peak,
-                         "spec_ops_per_candidate": work.per_candidate(wkey, "spec")},
+                         "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
+                         "lds_cycle_frac": work.lds_frac(wkey, per_launch / (avg_launch_ms / 1e3))},
             "cpu_baseline": cpu,
             "per_format": side,
             "lowest_hit_index": None if lowest is None or lowest >= (1 << 62) else lowest,
