@@ -1,0 +1,70 @@
+"""The per-candidate primitive counts behind bench.py's roofline (dprf_amd/work.py COUNTS) against the
+oracle's own counters (oracle.c orc_work_counts, which counts every compression, block and KSA the
+restated reference verifiers run), and the LDS cycle model of the RC4 formats against its derivation."""
+import random
+
+import pytest
+
+from dprf_amd import work
+
+
+def _counts(oracle, streams, name, pw):
+    return {k: v for k, v in oracle.Ctx(streams[name]["stream"]).work_counts(pw).items() if v}
+
+
+def test_office_counts(oracle, streams):
+    c = _counts(oracle, streams, "office_testdoc", "abcd")      # wrong password: no verifier hash
+    w = work.COUNTS["office"]
+    assert c["sha1c"] == w["sha1c_office_loop"] + w["sha1c"]
+    assert c["aes128_key_exp"] == w["aes128_keyexp"]
+
+
+@pytest.mark.parametrize("name,key", [("odt_testdoc_std", "odt"), ("odt_testdoc_e", "odt_e")])
+def test_odt_counts(oracle, streams, name, key):
+    c = _counts(oracle, streams, name, "abcd")
+    w = work.COUNTS[key]
+    assert c["sha1c"] == w["sha1c"] + w["sha1c_hmac20"]
+    assert c["sha256c"] == w["sha256c"]
+    assert c["aes256_dec_blocks"] == w["aes256_dec_block"]
+
+
+def test_pdf_rc4_counts(oracle, streams):
+    c = _counts(oracle, streams, "pdf_testdoc_r4", "abcdefg")
+    w = work.COUNTS["pdf_r34"]
+    # the reference recomputes the document-constant MD5(PAD || ID) per candidate (:167); COUNTS does not
+    assert c["md5c"] == w["md5c"] + w["md5c_16"] + 1
+    assert c["rc4_ksa"] == w["rc4_ksa"] and c["rc4_prga_bytes"] == w["rc4_prga_byte"]
+    c = _counts(oracle, streams, "pdf_testdoc_r2", "abcdefg")
+    w = work.COUNTS["pdf_r2"]
+    assert c["md5c"] == w["md5c"] and c["rc4_ksa"] == w["rc4_ksa"] and c["rc4_prga_bytes"] == w["rc4_prga_byte"]
+
+
+def test_pdf_r5_counts(oracle, streams):
+    assert _counts(oracle, streams, "pdf_synth_r5_cat", "abcdefg") == {"sha256c": work.COUNTS["pdf_r5"]["sha256c"]}
+
+
+def test_pdf_r6_mean_counts(oracle, streams):
+    """COUNTS["pdf_r6"] is a mean over random 6-letter candidates; 300 others land within 3 %."""
+    rng = random.Random(1)
+    ctx = oracle.Ctx(streams["pdf_synth_r6_ox"]["stream"])
+    tot = {}
+    n = 300
+    for _ in range(n):
+        pw = "".join(rng.choice("abcdefghijklmnopqrstuvwxyz") for _ in range(6))
+        for k, v in ctx.work_counts(pw).items():
+            tot[k] = tot.get(k, 0) + v / n
+    w = work.COUNTS["pdf_r6"]
+    for ok, wk in [("sha256c", "sha256c"), ("sha512c", "sha512c"), ("aes128_enc_blocks", "aes128_enc_block"),
+                   ("aes128_key_exp", "aes128_keyexp")]:
+        assert abs(tot[ok] - w[wk]) / w[wk] < 0.03, ok
+
+
+def test_lds_cycle_model():
+    # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (2 + 4 + 4) + 63 dword reads x 2 + PRGA-2: 5 x 2 + 2 x 4)
+    assert work.LDS_CYCLES["pdf_r34"] * 64 == 20 * (64 * 2 + 256 * 10 + 63 * 2 + 5 * 2 + 2 * 4)
+    # R2: 64 ds_write_b32 x 4 + 256 x (2 reads + 2 stores) - last S[i+1] read + 32 x (3 reads + 2 stores)
+    assert work.LDS_CYCLES["pdf_r2"] * 64 == 64 * 4 + 256 * (2 * 2 + 2 * 4) - 2 + 32 * (3 * 2 + 2 * 4)
+    assert work.lds_frac("odt", 1e6) is None
+    assert abs(work.lds_frac("pdf_r34", 1e6) - 1e6 * work.LDS_CYCLES["pdf_r34"] / (256 * 2.4e9)) < 1e-12
+    for fmt in work.LDS_CYCLES:
+        assert work.BOUND[fmt] == "lds"
