@@ -326,7 +326,9 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #define R6_LANES 768
 #endif
 #define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
+#ifndef R6_MAX_SLOTS
 #define R6_MAX_SLOTS 1280
+#endif
 #define R6_CLASSES 7                    /* 6 live classes + "no candidate" */
 #define R6_IDLE 0xffffffffu
 #define R6_MAX_BATCHES (R6_MAX_SLOTS / 64 + 2)
