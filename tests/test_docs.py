@@ -95,3 +95,59 @@ def test_brute_force_cli_recovers_document_passwords(docs):
         with contextlib.redirect_stdout(io.StringIO()):
             found, pw = brute_force.main([doc_type, os.path.join(DOCS, name), "-pr", "3"])
         assert (found, pw) == (1, e["password"]), name
+
+
+RANDOM_DOCS = [("docx", {}), ("odt", {}), ("pdf", {"R": 2, "length": 40}), ("pdf", {"R": 3, "length": 128}),
+               ("pdf", {"R": 3, "length": 40}), ("pdf", {"R": 4, "length": 128, "meta": False}),
+               ("pdf", {"R": 5, "length": 256}), ("pdf", {"R": 6, "length": 256})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,kw", RANDOM_DOCS, ids=lambda v: v if isinstance(v, str) else
+                         "-".join("%s%s" % kv for kv in sorted(v.items())))
+def test_gpu_random_documents_vs_oracle(oracle, kind, kw):
+    """Documents with fresh random salts / IDs / IVs and a random [a-z]^3 password (seeded, written by
+    tests/docgen.py and parsed by dprf_amd/parsers): the GPU hit set over the whole [a-z]^3 keyspace holds
+    the password and the oracle confirms every hit; the oracle's own scan of the keyspace equals it where
+    that takes well under a second (PDF R2-R5), elsewhere 300 random non-hits are confirmed as misses."""
+    import random
+    import zlib
+    import docgen
+    from dprf_amd import _lib
+    from dprf_amd.parsers import odt2hashes, office2john, pdf2john
+    rng = random.Random(zlib.crc32(repr((kind, sorted(kw.items()))).encode()))
+    full_scan = kind == "pdf" and kw["R"] <= 5
+    with tempfile.TemporaryDirectory() as t:
+        for trial in range(2):
+            pw = "".join(rng.choice(LOWER) for _ in range(3))
+            seed = rng.randrange(1 << 30)
+            path = os.path.join(t, "doc%d.%s" % (trial, kind))
+            if kind == "docx":
+                docgen.write_docx(path, pw, seed)
+                streams = [office2john.get_hash(path)]
+            elif kind == "odt":
+                docgen.write_odt(path, pw, seed)
+                streams = [odt2hashes.get_hashes(path, False), odt2hashes.get_hashes(path, True)]
+            else:
+                docgen.write_pdf(path, pw, seed, **kw)
+                streams = [pdf2john.get_hash(path)]
+            idx = 0
+            for ch in pw:
+                idx = idx * 26 + LOWER.index(ch)
+            for stream in streams:
+                octx = oracle.Ctx(stream)
+                with _lib.Context(_fields(stream), device=0) as ctx:
+                    hits, n, st = ctx.search_range(LOWER, 3, 0, 26 ** 3)
+                assert st["candidates"] == 26 ** 3 and n == len(hits)
+                assert idx in hits, (kind, kw, pw, seed)
+                word = lambda h: (LOWER[h // 676] + LOWER[h // 26 % 26] + LOWER[h % 26]).encode()
+                for h in hits:
+                    assert octx.verify(word(h)) == 1, (kind, kw, h)
+                if full_scan:
+                    want, _ = octx.search_range(LOWER, 3, 0, 26 ** 3)
+                    assert hits == want, (kind, kw, pw, seed)
+                else:
+                    hs = set(hits)
+                    for h in rng.sample(range(26 ** 3), 300):
+                        if h not in hs:
+                            assert octx.verify(word(h)) == 0, (kind, kw, h)
