@@ -414,6 +414,30 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
  * the block prologue were a third of the kernel (2 Mi waves per 128 Mi-candidate launch).  Each thread
  * now takes R5_PER candidates, 256 apart. */
 #define R5_PER 8
+/* SHA-256 of one block from the IV, compared with u[0:8], with an early exit: the last word of the digest
+ * is IV7 + (e after round 60) -- that e only moves down to h in rounds 61-63 -- so a wave none of whose
+ * lanes matches u[7] there (all but a 2^-32 fraction) skips rounds 61-63 and their schedule words. */
+DEVI bool sha256_block_matches(uint32_t w[16], const uint32_t u[8], bool valid) {
+    uint32_t a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
+    uint32_t e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        if (t == 61 && !__builtin_amdgcn_ballot_w64(valid && e + 0x5be0cd19u == u[7])) return false;
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = w[t & 15] + s0_256(w[(t - 15) & 15]) + w[(t - 7) & 15] + s1_256(w[(t - 2) & 15]);
+            w[t & 15] = wt;
+        }
+        const uint32_t t1 = h + S1_256(e) + f_ch(e, f, g) + (k256(t) + wt);
+        const uint32_t t2 = S0_256(a) + f_maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    return valid && a + 0x6a09e667u == u[0] && b + 0xbb67ae85u == u[1] && c + 0x3c6ef372u == u[2] &&
+           d + 0xa54ff53au == u[3] && e + 0x510e527fu == u[4] && f + 0x9b05688cu == u[5] &&
+           g + 0x1f83d9abu == u[6] && h + 0x5be0cd19u == u[7];
+}
 template <int MODE>
 __global__ void __launch_bounds__(256)
 k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
@@ -457,13 +481,7 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
             uint32_t b[16];
 #pragma unroll
             for (int j = 0; j < 16; j++) b[j] = (j < DPRF_MAX_RANGE_LEN / 4 ? bswap32(c.w[j]) : 0u) | tail[j];
-            uint32_t hh[8];
-            sha256_iv(hh);
-            sha256_compress(hh, b);
-            bool ok = true;
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) ok = ok && hh[kk] == p.u[kk];
-            if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+            if (sha256_block_matches(b, p.u, valid)) report_hit(R, e.start + g, cap, stop_on_first);
             continue;
         }
         /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
