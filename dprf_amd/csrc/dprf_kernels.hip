@@ -658,6 +658,22 @@ DEVI void rc4_ksa_ahead(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     lds_st8(S, rc4_addr(pj, lanebase), ps);
 }
 /* PRGA of NB bytes XORed into d[] (LE-packed). */
+/* PRGA bytes FROM..TO (1-based keystream positions), j carried in and out, XORed into d[] (LE-packed) */
+template <int FROM, int TO>
+DEVI void rc4_prga_span(uint8_t *S, uint32_t lanebase, uint32_t d[], uint32_t &j) {
+#pragma unroll
+    for (int i = FROM; i <= TO; i++) {
+        const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
+        const uint32_t si = lds_ld8(S, ai);
+        j = j + si;
+        const uint32_t aj = rc4_addr(j, lanebase);
+        const uint32_t sj = lds_ld8(S, aj);
+        lds_st8(S, ai, sj);
+        lds_st8(S, aj, si);
+        const uint32_t ks = lds_ld8(S, rc4_addr(si + sj, lanebase));
+        d[(i - 1) >> 2] ^= ks << (8 * ((i - 1) & 3));
+    }
+}
 template <int NB>
 DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
     uint32_t j = 0;
@@ -824,10 +840,24 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
             rc4_ksa_ahead<5>(Sw, lanebase, h);
+#ifndef DPRF_R2_FULL_PRGA
+            /* the first 4 keystream bytes decide for all but a 2^-32 fraction of the lanes: the wave
+             * continues the same keystream (i = 5.., j carried) only when one of its lanes matches U[0:4] */
+            uint32_t jj = 0;
+            rc4_prga_span<1, 4>(Sw, lanebase, d, jj);
+            ok = false;
+            if (__builtin_amdgcn_ballot_w64(valid && d[0] == p.u[0])) {
+                rc4_prga_span<5, 32>(Sw, lanebase, d, jj);
+                ok = true;
+#pragma unroll
+                for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
+            }
+#else
             rc4_prga<32>(Sw, lanebase, d);
             ok = true;
 #pragma unroll
             for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
+#endif
         } else {
             /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
             for (uint32_t full = 0; full < 2u; full++) {
