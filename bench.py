@@ -189,6 +189,9 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
     _, cs, pwlen, B, _, _ = WORKLOADS[name]
     B = batch or B
     space = len(cs) ** pwlen
+    while space < world * B:     # e.g. Office -pr 4 (one batch) at N > 1: the next length keeps the shards disjoint
+        pwlen += 1
+        space = len(cs) ** pwlen
     stats = []
     lowest = None
 
@@ -208,7 +211,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
         lowest = low if lowest is None else min(lowest, low)
     sync()
     dt = time.perf_counter() - t0
-    return dt, stats, lowest
+    return dt, stats, lowest, pwlen
 
 
 def main():
@@ -266,7 +269,7 @@ def main():
 
     ctx = _lib.Context(fields, device=local)
     B = args.batch or B
-    dt, stats, lowest = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync, allreduce_min, B)
+    dt, stats, lowest, pwlen = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync, allreduce_min, B)
     dt_max = allreduce_max(dt)
     cands = sum(s["candidates"] for s in stats)
     total = cands * world
@@ -291,12 +294,13 @@ def main():
             sn, scs, spl, sB, skey, sdesc = WORKLOADS[name]
             sf = quiet_fields(brute_force, S[sn]["stream"])
             sctx = _lib.Context(sf, device=local)
-            sdt, sst, _ = run_workload(name, sctx, rank, world, 2, 1, sync, allreduce_min)
+            sdt, sst, _, spl = run_workload(name, sctx, rank, world, 2, 1, sync, allreduce_min)
             sdt = allreduce_max(sdt)
             sc = sum(s["candidates"] for s in sst)
             sl = sum(s["launches"] for s in sst)
             skm = sum(s["kernel_ms"] for s in sst)
             side[name] = {"value": sc * world / sdt, "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
+                          "pwlen": spl,
                           "avg_launch_ms": skm / max(1, sl),
                           "valu_floor_frac": (sc / max(1, sl)) * work.per_candidate(skey) / (skm / max(1, sl) / 1e3) / peak}
             if work.BOUND.get(skey) == "lds":

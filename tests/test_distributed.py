@@ -72,3 +72,29 @@ def test_brute_force_round_slices_tile_the_block():
             for (a, n), (b, _) in zip(sl, sl[1:]):
                 assert a + n == b
             assert sum(n for _, n in sl) == block
+
+
+def test_small_keyspace_shards_stay_disjoint_at_eight_ranks():
+    """Office -pr 4 is one batch: at N > 1 bench.run_workload moves to the next length so the ranks'
+    slices of every step are disjoint instead of all ranks verifying the same candidates."""
+    import bench
+
+    seen = {}
+
+    class FakeCtx:
+        def __init__(self, rank):
+            self.rank = rank
+
+        def search_range(self, cs, pwlen, start, n):
+            seen.setdefault(pwlen, []).append((start, n))
+            return [], 0, {"candidates": n}
+
+    world = 8
+    for rank in range(world):
+        _, _, _, pwlen = bench.run_workload("office", FakeCtx(rank), rank, world, 2, 1, lambda: None, lambda v: v)
+        assert pwlen == 5
+    spans = sorted(seen[5])
+    assert len(spans) == 3 * world
+    for (s0, n0), (s1, _) in zip(spans, spans[1:]):
+        assert s0 + n0 <= s1
+    assert all(n == 26 ** 4 for _, n in spans)
