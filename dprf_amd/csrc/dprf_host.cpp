@@ -641,6 +641,7 @@ extern "C" int dprf_verify_list(dprf_ctx *c, const uint8_t *blob, const uint64_t
                        e.start = off;
                        e.count = cnt;
                        e.mode = 1;
+                       e.pwlen = *std::max_element(lens.begin() + (ptrdiff_t)off, lens.begin() + (ptrdiff_t)(off + cnt));
                        e.slots = c->d_slots;
                        e.lens = c->d_lens;
                    },

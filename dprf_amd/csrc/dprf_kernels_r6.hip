@@ -546,7 +546,9 @@ static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots
 
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
-    const uint32_t lmax = e.mode == 0 ? e.pwlen : 4u * DPRF_SLOT_WORDS;
+    /* longest password of the launch (list mode: the host's maximum over the chunk): the period length
+     * and with it the slots per CU follow the actual candidates, not the 64-byte slot width */
+    const uint32_t lmax = e.pwlen < 4u * DPRF_SLOT_WORDS ? e.pwlen : 4u * DPRF_SLOT_WORDS;
     /* period (lmax + 64) + 16 wrap bytes, + 4 words read past the last block start */
     const uint32_t pat_words = (lmax + 64u + 16u + 3u) / 4u + 1u;
     uint32_t nslots = 0, te_slots = 0;

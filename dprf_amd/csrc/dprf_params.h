@@ -16,7 +16,7 @@ struct dprf_enum {
     uint64_t start;
     uint32_t count;
     uint32_t mode;                  /* 0 range, 1 list */
-    uint32_t pwlen;                 /* range: fixed length (bytes) */
+    uint32_t pwlen;                 /* range: fixed length (bytes); list: longest candidate of the launch */
     uint32_t cslen;
     uint32_t div_m;                 /* u32 division by cslen: q = (mulhi(n,m) + ((n-mulhi)>>1)) >> s */
     uint32_t div_s;
