@@ -20,7 +20,6 @@ import ctypes
 import json
 import os
 import sys
-import threading
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -47,7 +46,7 @@ WORKLOADS = {
 # rocprofv3 name of the dominant kernel per libdprf kernel family (the one "roofline" times)
 DOMINANT = {"office_std": "k_office_kdf", "odf_aes256": "k_odt_kdf", "pdf_r24": "k_pdf_r24", "pdf_r5": "k_pdf_r5",
             "pdf_r6": "k_pdf_r6"}
-SIDE_FORMATS = ["office", "pdf_r34", "pdf_r6", "pdf_r2", "pdf_r5"]
+SIDE_FORMATS = ["office", "odt_e", "pdf_r34", "pdf_r6", "pdf_r2", "pdf_r5"]
 
 
 def streams():
@@ -136,9 +135,32 @@ def _popen_worker(job):
     return n
 
 
+def cpu_share():
+    """(nproc, cores this job may use).  On the GPU box nproc is the whole machine while the job's share is
+    16 CPUs (the pool's rule; exported there as OMP_NUM_THREADS), so the share is the cgroup CPU quota if
+    one is set, else OMP_NUM_THREADS, else the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = aff
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            share = min(share, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    else:
+        if q == "max" and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    return os.cpu_count() or aff, max(1, share)
+
+
 def reference_process_model(fields, charset, pwlen, seconds=2.0, procs=4):
     """The reference engine's own cost structure: 4 worker processes (brute_force.py:70-73), one fork/exec
-    of the compiled reference verifier per candidate.  Python 3 drives it (there is no Python 2.7 here)."""
+    of the compiled reference verifier per candidate (brute_force.py:123-140, 163-197).  Python 3 drives it
+    (there is no Python 2.7 here)."""
     import multiprocessing as mp
     exe = os.path.join(HERE, "oracle", "_ref", {"office": "msoffcrypto", "odt": "odt", "pdf": "pdf"}[fields[0]])
     if not os.path.exists(exe):
@@ -154,16 +176,12 @@ def reference_process_model(fields, charset, pwlen, seconds=2.0, procs=4):
 
 
 def cpu_baseline(fields, charset, pwlen, seconds=1.5, procs=None):
-    """The reference's verify() on the host cores, one worker PROCESS per core (the reference's own process
-    model, brute_force.py:70-73, minus its per-candidate fork/exec), for a bounded time over the first
-    indices of the workload keyspace.  Run before anything touches the GPU (workers are spawned)."""
+    """The reference's verify() on `procs` worker PROCESSES (the reference's own process model,
+    brute_force.py:70-73, minus its per-candidate fork/exec), for a bounded time over the first indices of
+    the workload keyspace.  Run before anything touches the GPU (workers are spawned)."""
     import multiprocessing as mp
     kind = "reference" if ref_callable(fields) is not None else "port"
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    procs = procs or max(1, min(16, ncpu))
+    procs = procs or cpu_share()[1]
     with mp.get_context("spawn").Pool(procs) as pool:
         pool.map(_cpu_worker, [(fields, charset, pwlen, t, procs, time.time() + 0.2) for t in range(procs)])  # warm
         t0 = time.time()
@@ -171,9 +189,24 @@ def cpu_baseline(fields, charset, pwlen, seconds=1.5, procs=None):
         dt = time.time() - t0
     n = sum(counts)
     return {"value": n / dt, "unit": "candidates/s", "cores": procs, "kind": kind,
-            "sample": "%d candidates (the first indices of the workload keyspace) in %.1f s on %d worker processes: "
+            "sample": "%d candidates (the first indices of the workload keyspace) in %.1f s on %d worker process%s: "
                       "the reference's verify() %s in-process, no per-candidate fork/exec" % (
-                          n, dt, procs, "compiled from /root/reference" if kind == "reference" else "(C port)")}
+                          n, dt, procs, "" if procs == 1 else "es",
+                          "compiled from /root/reference" if kind == "reference" else "(C port)")}
+
+
+def cpu_baselines(fields, charset, pwlen, seconds=1.5, process_model=True):
+    """SURVEY.md 8(d) CPU path: the reference's verify() on 1 worker, on all cores of this job's share, and
+    the reference's 4-process Popen-per-candidate model, with nproc and the share stated.  `value` is the
+    all-cores figure."""
+    nproc, share = cpu_share()
+    allc = cpu_baseline(fields, charset, pwlen, seconds=seconds, procs=share)
+    one = cpu_baseline(fields, charset, pwlen, seconds=seconds, procs=1)
+    out = dict(allc)
+    out.update({"nproc": nproc, "cpu_share": share, "all_cores": allc, "one_worker": one})
+    if process_model:
+        out["process_model_4"] = reference_process_model(fields, charset, pwlen, seconds=seconds)
+    return out
 
 
 # ------------------------------------------------------------------ GPU timing
@@ -185,9 +218,14 @@ def shard(step, rank, world, batch, space):
     return start, min(batch, space - start)
 
 
-def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, batch=None):
+def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, batch=None, ndev=1):
+    """W untimed + K timed steps of `name` on this rank.  A step verifies B consecutive indices per GPU
+    (ndev GPUs in this process: one multi-device library call covers ndev * B) through
+    brute_force.search_round -- the exact call the product's range mode makes per round -- then the ranks
+    all-reduce (MIN) the lowest hit index, the early-stop exchange of a sharded search."""
+    from dprf_amd import brute_force
     _, cs, pwlen, B, _, _ = WORKLOADS[name]
-    B = batch or B
+    B = (batch or B) * ndev
     space = len(cs) ** pwlen
     while space < world * B:     # e.g. Office -pr 4 (one batch) at N > 1: the next length keeps the shards disjoint
         pwlen += 1
@@ -197,9 +235,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
 
     def step(s):
         start, n = shard(s, rank, world, B, space)
-        hits, _, st = ctx.search_range(cs, pwlen, start, n)
-        first = hits[0] if hits else (1 << 62)
-        return allreduce_min(first), st
+        idx, st = brute_force.search_round(ctx, cs, pwlen, start, n)
+        return allreduce_min(idx if idx is not None else (1 << 62)), st
 
     for s in range(warmup):
         step(s)
@@ -212,6 +249,34 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
     sync()
     dt = time.perf_counter() - t0
     return dt, stats, lowest, pwlen
+
+
+def pmc_summary(workload):
+    """rocprof-derived counters of the workload's dominant kernel (profiles/pmc_valu.json, written by
+    tools/pmc_valu.py from the tools/profile_gpu.sh passes): VALUBusy, VALUUtilization, LDS busy."""
+    p = os.path.join(HERE, "profiles", "pmc_valu.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p)).get(workload)
+
+
+def summarize(stats, wkey, world, dt):
+    from dprf_amd import work
+    cands = sum(s["candidates"] for s in stats)
+    launches = sum(s["launches"] for s in stats)
+    kern_ms = sum(s["kernel_ms"] for s in stats)
+    main_ms = sum(s["main_kernel_ms"] for s in stats)
+    wall_ms = sum(s["wall_ms"] for s in stats)
+    devs = max(1, max(s.get("devices", 1) for s in stats))
+    avg_launch_ms = main_ms / max(1, launches)
+    per_launch = cands / max(1, launches)
+    floor = work.per_candidate(wkey, part="main")
+    achieved = per_launch * floor / (avg_launch_ms / 1e3)
+    return {"cands": cands, "launches": launches, "kern_ms": kern_ms, "avg_launch_ms": avg_launch_ms,
+            "per_launch": per_launch, "floor": floor, "achieved": achieved,
+            # host time of the library calls not covered by device time (launch gaps, polling, hit merge)
+            "call_overhead": 1.0 - kern_ms / max(1e-9, wall_ms * devs),
+            "value": cands * world / dt}
 
 
 def main():
@@ -235,9 +300,17 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    # one process per GPU under torchrun (world = N); `--gpus N` without a launcher drives N GPUs from this
+    # one process through one multi-device library context instead
+    devices = [local]
+    if world == 1 and args.gpus > 1:
+        devices = _lib.device_list()[:args.gpus]
+        if len(devices) < args.gpus:
+            raise SystemExit("--gpus %d: only %d gfx950 devices visible" % (args.gpus, len(devices)))
 
     def sync():
-        torch.cuda.synchronize(dev)
+        for d in devices:
+            torch.cuda.synchronize(torch.device("cuda", d))
         if dist:
             dist.barrier()
 
@@ -258,33 +331,36 @@ def main():
     S = streams()
     stream_name, cs, pwlen, B, wkey, desc = WORKLOADS[args.workload]
     fields = quiet_fields(brute_force, S[stream_name]["stream"])
+    n_gpus = world * len(devices)
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(fields, cs, pwlen, seconds=args.cpu_seconds)
-        pm = reference_process_model(fields, cs, pwlen)
-        if pm:
-            cpu["reference_process_model"] = pm
+    side_cpu = {}
+    if rank == 0 and n_gpus == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baselines(fields, cs, pwlen, seconds=args.cpu_seconds)
         log("cpu baseline:", cpu)
+        if not args.no_side:
+            for name in SIDE_FORMATS:
+                if name == args.workload:
+                    continue
+                sn, scs, spl, _, _, _ = WORKLOADS[name]
+                sf = quiet_fields(brute_force, S[sn]["stream"])
+                # configs[0] IS "brute_force.py on CPU": Office gets the full set (1 worker, 4-process model)
+                side_cpu[name] = (cpu_baselines(sf, scs, spl, seconds=min(1.0, args.cpu_seconds))
+                                  if name == "office" else
+                                  cpu_baseline(sf, scs, spl, seconds=min(1.0, args.cpu_seconds)))
 
-    ctx = _lib.Context(fields, device=local)
+    ctx = _lib.Context(fields, devices=devices)
     B = args.batch or B
-    dt, stats, lowest, pwlen = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync, allreduce_min, B)
+    dt, stats, lowest, pwlen = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync,
+                                            allreduce_min, B, ndev=len(devices))
     dt_max = allreduce_max(dt)
-    cands = sum(s["candidates"] for s in stats)
-    total = cands * world
-    launches = sum(s["launches"] for s in stats)
-    kern_ms = sum(s["kernel_ms"] for s in stats)
-    main_ms = sum(s["main_kernel_ms"] for s in stats)
-    avg_launch_ms = main_ms / max(1, launches)          # dominant kernel alone (Office/ODF: the KDF kernel)
-    per_launch = cands / max(1, launches)
-    floor = work.per_candidate(wkey, part="main")
-    achieved = per_launch * floor / (avg_launch_ms / 1e3)
+    m = summarize(stats, wkey, world, dt_max)
     peak = work.PEAK_LANE_INSTR_PER_S
     traffic = None
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         traffic = json.load(open(pmc)).get(args.workload, {}).get("bytes_per_launch")
+    counters = pmc_summary(args.workload)
 
     side = {}
     if not args.no_side:
@@ -293,26 +369,47 @@ def main():
                 continue
             sn, scs, spl, sB, skey, sdesc = WORKLOADS[name]
             sf = quiet_fields(brute_force, S[sn]["stream"])
-            sctx = _lib.Context(sf, device=local)
-            sdt, sst, _, spl = run_workload(name, sctx, rank, world, 2, 1, sync, allreduce_min)
+            sctx = _lib.Context(sf, devices=devices)
+            sdt, sst, _, spl = run_workload(name, sctx, rank, world, 2, 1, sync, allreduce_min, ndev=len(devices))
             sdt = allreduce_max(sdt)
-            sc = sum(s["candidates"] for s in sst)
-            sl = sum(s["launches"] for s in sst)
-            skm = sum(s["kernel_ms"] for s in sst)
-            side[name] = {"value": sc * world / sdt, "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
-                          "pwlen": spl,
-                          "avg_launch_ms": skm / max(1, sl),
-                          "valu_floor_frac": (sc / max(1, sl)) * work.per_candidate(skey) / (skm / max(1, sl) / 1e3) / peak}
+            sm = summarize(sst, skey, world, sdt)
+            side[name] = {"value": sm["value"], "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
+                          "pwlen": spl, "bound": work.BOUND.get(skey, "valu"),
+                          "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
+                          "valu_floor_frac": (sm["per_launch"] * work.per_candidate(skey)
+                                              / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak),
+                          "call_overhead": sm["call_overhead"]}
             if work.BOUND.get(skey) == "lds":
-                side[name]["lds_cycle_frac"] = work.lds_frac(skey, (sc / max(1, sl)) / (skm / max(1, sl) / 1e3))
+                side[name]["lds_cycle_frac"] = work.lds_frac(
+                    skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
+            pc = pmc_summary(name)
+            if pc:
+                side[name]["rocprof"] = pc
+            if name in side_cpu:
+                side[name]["cpu_baseline"] = side_cpu[name]
             sctx.close()
 
     if rank == 0:
+        roof = {"bound": work.BOUND.get(wkey, "valu"), "achieved": m["achieved"] / 1e12, "peak": peak / 1e12,
+                "unit": "T VALU lane-slots/s (gfx950 issue-slot floor of the algorithm)",
+                "frac": m["achieved"] / peak, "traffic": traffic,
+                "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),
+                "kernel_avg_ms": m["avg_launch_ms"], "candidates_per_launch": m["per_launch"],
+                "floor_instr_per_candidate": m["floor"],
+                "all_kernels_avg_ms": m["kern_ms"] / max(1, m["launches"]),
+                "all_kernels_frac": m["cands"] * work.per_candidate(wkey) / (m["kern_ms"] / 1e3) / peak,
+                "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
+                "lds_cycle_frac": work.lds_frac(wkey, m["per_launch"] / (m["avg_launch_ms"] / 1e3)),
+                "call_overhead": m["call_overhead"]}
+        if counters:
+            roof["valu_busy"] = counters.get("valu_busy")
+            roof["valu_utilization"] = counters.get("valu_utilization")
+            roof["rocprof"] = counters
         out = {
             "metric": METRIC,
-            "value": total / dt_max,
+            "value": m["cands"] * world / dt_max,
             "unit": "candidates/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt_max / args.steps * 1e3,
@@ -324,17 +421,11 @@ def main():
                     "reference's test document",
             "config": {"workload": args.workload, "description": desc, "document": stream_name,
                        "charset": "alnum (a-z A-Z 0-9)" if cs == ALNUM else "lowercase", "pwlen": pwlen,
-                       "batch_per_gpu": B, "kernel": ctx.kernel, "parallelism": "keyspace shards x%d" % world},
-            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": peak / 1e12,
-                         "unit": "T VALU lane-instr/s (gfx950 instruction floor of the algorithm)",
-                         "frac": achieved / peak, "traffic": traffic,
-                         "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),
-                         "kernel_avg_ms": avg_launch_ms, "candidates_per_launch": per_launch,
-                         "floor_instr_per_candidate": floor,
-                         "all_kernels_avg_ms": kern_ms / max(1, launches),
-                         "all_kernels_frac": cands * work.per_candidate(wkey) / (kern_ms / 1e3) / peak,
-                         "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
-                         "lds_cycle_frac": work.lds_frac(wkey, per_launch / (avg_launch_ms / 1e3))},
+                       "batch_per_gpu": B, "kernel": ctx.kernel,
+                       "parallelism": "keyspace shards x%d (%s)" % (
+                           n_gpus, "one process per GPU" if world > 1 else
+                           "one process, %d-device library context" % len(devices))},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "per_format": side,
             "lowest_hit_index": None if lowest is None or lowest >= (1 << 62) else lowest,

@@ -10,14 +10,16 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+ALL_DEVICES = -1
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
 FLAG_NEVER_MATCHES, FLAG_REF_NONDETERMINISTIC = 1, 2
 MAX_PW, MAX_PW_RANGE = 64, 32
 
-EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_ctx_create", "dprf_ctx_destroy",
-           "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel", "dprf_search_range", "dprf_verify_list"]
+EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_device_list", "dprf_ctx_create",
+           "dprf_ctx_create_devices", "dprf_ctx_destroy", "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel",
+           "dprf_ctx_devices", "dprf_search_range", "dprf_verify_list", "dprf_list_status"]
 
 
 class DprfError(RuntimeError):
@@ -28,11 +30,11 @@ class DprfError(RuntimeError):
 
 class Stats(ctypes.Structure):
     _fields_ = [("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
-                ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("devices", ctypes.c_uint32),
                 ("main_kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _lib = None
@@ -54,6 +56,15 @@ def lib():
             L.dprf_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]
             L.dprf_ctx_create.restype = ctypes.c_int
+            L.dprf_ctx_create_devices.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                                  ctypes.POINTER(ctypes.c_void_p)]
+            L.dprf_ctx_create_devices.restype = ctypes.c_int
+            L.dprf_ctx_devices.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+            L.dprf_device_list.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+            L.dprf_list_status.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.c_int64, ctypes.POINTER(ctypes.c_int8)]
+            L.dprf_list_status.restype = ctypes.c_int
             L.dprf_ctx_destroy.argtypes = [ctypes.c_void_p]
             L.dprf_ctx_format.argtypes = [ctypes.c_void_p]
             L.dprf_ctx_flags.argtypes = [ctypes.c_void_p]
@@ -83,22 +94,40 @@ def device_count():
     return lib().dprf_device_count()
 
 
+def device_list():
+    """HIP ordinals of the visible gfx950 devices (not simply range(device_count()): a non-gfx950 device
+    may sit at any ordinal)."""
+    arr = (ctypes.c_int * 64)()
+    n = lib().dprf_device_list(arr, 64)
+    return list(arr[:min(n, 64)])
+
+
 def _to_bytes(p):
     return p.encode("utf-8") if isinstance(p, str) else bytes(p)
 
 
 class Context:
-    """One document on one GPU: the compiled form of the verifier argv brute_force.py builds per
-    candidate (brute_force.py:163-197)."""
+    """One document on one or more GPUs: the compiled form of the verifier argv brute_force.py builds per
+    candidate (brute_force.py:163-197).  ``devices``: a list of HIP ordinals (the library runs one worker
+    thread and one stream per entry and splits every call over them); ``device``: one ordinal, or
+    ALL_DEVICES for every gfx950 device."""
 
-    def __init__(self, fields, device=0):
+    def __init__(self, fields, device=0, devices=None):
         fields = list(fields)
         arr = (ctypes.c_char_p * len(fields))(*[_to_bytes(f) for f in fields])
         h = ctypes.c_void_p()
-        _check(lib().dprf_ctx_create(arr, len(fields), int(device), ctypes.byref(h)))
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            darr = (ctypes.c_int * max(1, len(devs)))(*devs)
+            _check(lib().dprf_ctx_create_devices(arr, len(fields), darr, len(devs), ctypes.byref(h)))
+        else:
+            _check(lib().dprf_ctx_create(arr, len(fields), int(device), ctypes.byref(h)))
         self._h = h
         self.fields = fields
-        self.device = device
+        out = (ctypes.c_int * 64)()
+        n = lib().dprf_ctx_devices(h, out, 64)
+        self.devices = list(out[:min(n, 64)])
+        self.device = self.devices[0]
 
     def close(self):
         if getattr(self, "_h", None):
@@ -154,6 +183,19 @@ class Context:
         _check(lib().dprf_verify_list(self._h, bytes(blob), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                       n, 1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
         return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()
+
+    def list_status(self, blob, offsets):
+        """Per-candidate validity for this format without device work: a numpy int8 array, 0 = valid,
+        else the DPRF_E_* code verify_blob would fail the whole payload with."""
+        import numpy as np
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offs) - 1
+        st = np.zeros(max(1, n), dtype=np.int8)
+        rc = lib().dprf_list_status(self._h, bytes(blob), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n,
+                                    st.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
+        if rc < 0:
+            _check(rc)
+        return st[:n]
 
     def verify_list(self, passwords, stop_on_first=False, cap=1 << 16):
         """Verify an explicit candidate list (a client payload).  Returns (sorted hit list indices,

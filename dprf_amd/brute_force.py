@@ -21,12 +21,16 @@ candidates go to libdprf.so in batches, one candidate per GPU lane.  Differences
 * optional keyword arguments ``charset`` (default lowercase a-z, Python 2 ``string.lowercase`` in the C
   locale), ``devices`` (default: every visible gfx950 GPU) and ``checkpoint`` (a resumable cursor file
   for range mode, :class:`Checkpoint`).
+
+The reference's four worker processes on one queue (:70-73, :92-95) are inside libdprf.so: one context
+spans the devices, and every search call fans out over them (one worker thread + HIP stream per GPU on a
+shared chunk cursor, include/dprf.h).  Range mode calls it in rounds of about ROUND_SECONDS of work so the
+checkpoint cursor advances and Ctrl-C is honoured between rounds.
 """
 import argparse
 import re
 import sys
 import textwrap
-import threading
 import time
 
 from . import _lib
@@ -35,7 +39,8 @@ LOWERCASE = "abcdefghijklmnopqrstuvwxyz"
 ALNUM = LOWERCASE + LOWERCASE.upper() + "0123456789"   # the configs' "alnum" order: a-z A-Z 0-9
 DEFAULT_PASSWORD = "default_password_allocation"
 DUMMY = "_dummy"
-ROUND_PER_DEVICE = 1 << 24      # candidates per device between stop checks in range mode
+ROUND_SECONDS = 5.0              # range mode: wall time of one library call (checkpoint / Ctrl-C granularity)
+FIRST_ROUND = 1 << 22           # candidates of the first round, before a rate is known
 
 
 def init(stream, password_range, passwords, charset=LOWERCASE, devices=None, checkpoint=None):
@@ -60,15 +65,16 @@ def init(stream, password_range, passwords, charset=LOWERCASE, devices=None, che
 
 def _devices(devices):
     if devices is None:
-        n = _lib.device_count()
-        if n < 1:
+        devs = _lib.device_list()
+        if not devs:
             raise _lib.DprfError(_lib.E_NODEVICE, "no gfx950 device visible")
-        return list(range(n))
+        return devs
     return list(devices)
 
 
-def _contexts(input_data, devices):
-    return [_lib.Context(input_data, device=d) for d in _devices(devices)]
+def _context(input_data, devices):
+    """One library context over the devices (the library splits every call over them)."""
+    return _lib.Context(input_data, devices=_devices(devices))
 
 
 def _report(found_pw, n, t0):
@@ -113,99 +119,74 @@ class Checkpoint:
         os.replace(tmp, self.path)
 
 
+def next_round(rate, remaining, seconds=ROUND_SECONDS):
+    """Candidates of the next range-mode round: ~`seconds` at the measured rate (cand/s; 0 = unknown)."""
+    n = FIRST_ROUND if rate <= 0 else max(FIRST_ROUND, int(rate * seconds))
+    return min(remaining, n)
+
+
+def search_round(ctx, charset, pwlen, start, count):
+    """One round of range mode on every device of ctx: (lowest hit index or None, stats).  The same call
+    bench.py times per rank."""
+    hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=True, cap=1)
+    return (hits[0] if hits else None), st
+
+
 def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, devices=None, checkpoint=None):
     """charset^password_range in product order, plus "_dummy" (brute_force.py:60-79, :199-219).
 
-    Multi-GPU: each round gives every device a contiguous slice of one contiguous block of the keyspace,
-    so after a round every index below the round's end has been verified and the lowest hit of the
-    first round that has one is the lowest hit overall.  checkpoint: path of a resumable cursor file
+    Rounds of consecutive indices, each one library call over all devices with stop_on_first: a round
+    returns its lowest hit, every index below a round's end has been verified once it returns, so the first
+    round with a hit holds the lowest hit overall.  checkpoint: path of a resumable cursor file
     (:class:`Checkpoint`)."""
     cp = Checkpoint(checkpoint, input_data, charset, password_range)
     done, prior = cp.load()
     if prior is not None:
         print("Checkpoint: search already finished, password '%s'" % prior)
         return 1, prior
-    ctxs = _contexts(input_data, devices)
+    ctx = _context(input_data, devices)
     t0 = time.time()
+    tried = 0
     try:
         if done == 0:
-            hits, _, _ = ctxs[0].verify_list([DUMMY], stop_on_first=True, cap=1)
+            hits, _, _ = ctx.verify_list([DUMMY], stop_on_first=True, cap=1)
+            tried += 1
             if hits:
                 cp.save(0, DUMMY)
-                _report(DUMMY, 1, t0)
+                _report(DUMMY, tried, t0)
                 return 1, DUMMY
         else:
             print("Checkpoint: resuming at index %d" % done)
         space = len(charset) ** password_range
-        found = None
+        found, rate = None, 0.0
         while done < space and found is None:
-            block = min(space - done, ROUND_PER_DEVICE * len(ctxs))
-            slices = _round_slices(done, block, len(ctxs))
-            results = [None] * len(ctxs)
-
-            def work(k):
-                s, n = slices[k]
-                results[k] = ctxs[k].search_range(charset, password_range, s, n, stop_on_first=True, cap=1) if n else ([], 0, {})
-
-            if len(ctxs) == 1:
-                work(0)
-            else:
-                ths = [threading.Thread(target=work, args=(k,)) for k in range(len(ctxs))]
-                [t.start() for t in ths]
-                [t.join() for t in ths]
-            firsts = [r[0][0] for r in results if r[0]]
-            if firsts:
-                idx = min(firsts)
+            n = next_round(rate, space - done)
+            idx, st = search_round(ctx, charset, password_range, done, n)
+            tried += st["candidates"]
+            rate = st["candidates"] / max(st["wall_ms"] / 1e3, 1e-9)
+            if idx is not None:
                 found = _index_to_password(idx, charset, password_range)
-            done += block
+            done += n
             cp.save(done, found)
-        _report(found, done + 1, t0)
+        _report(found, tried, t0)
         return (1, found) if found is not None else (0, DEFAULT_PASSWORD)
     finally:
-        for c in ctxs:
-            c.close()
-
-
-def _round_slices(done, block, ndev):
-    """Contiguous (start, count) slices, one per device, tiling [done, done + block)."""
-    per = -(-block // ndev)
-    out = []
-    for k in range(ndev):
-        s = done + k * per
-        out.append((min(s, done + block), max(0, min(per, done + block - s))))
-    return out
+        ctx.close()
 
 
 def init_listbased_brute_force(input_data, passwords, devices=None):
-    """An explicit candidate list, e.g. a server payload (brute_force.py:82-104).  The list is split
-    into contiguous slices, one per device; the lowest-index hit wins."""
+    """An explicit candidate list, e.g. a server payload (brute_force.py:82-104): one library call over all
+    devices; the lowest list index that verifies wins."""
     passwords = list(passwords)
-    ctxs = _contexts(input_data, devices)
+    ctx = _context(input_data, devices)
     t0 = time.time()
     try:
-        per = -(-len(passwords) // len(ctxs))
-        results = [None] * len(ctxs)
-
-        def work(k):
-            sl = passwords[k * per:(k + 1) * per]
-            results[k] = ctxs[k].verify_list(sl, stop_on_first=True, cap=1) if sl else ([], 0, {})
-
-        if len(ctxs) == 1:
-            work(0)
-        else:
-            ths = [threading.Thread(target=work, args=(k,)) for k in range(len(ctxs))]
-            [t.start() for t in ths]
-            [t.join() for t in ths]
-        found = None
-        for k, r in enumerate(results):
-            if r[0]:
-                found = passwords[k * per + r[0][0]]
-                break
+        hits, _, _ = ctx.verify_list(passwords, stop_on_first=True, cap=1)
+        found = passwords[hits[0]] if hits else None
         _report(found, len(passwords), t0)
         return (1, found) if found is not None else (0, DEFAULT_PASSWORD)
     finally:
-        for c in ctxs:
-            c.close()
+        ctx.close()
 
 
 def _index_to_password(idx, charset, n):

@@ -9,8 +9,8 @@
 * heartbeat thread: ``{"id"}`` to port 31337 every 20 s (client.py:101-116).
 
 The payload goes straight from the JSON text into libdprf's list mode (dprf_amd.payload.parse_message ->
-Context.verify_blob): no per-candidate Python, one context per (stream, GPU) kept across payloads,
-the payload split into contiguous slices over this client's GPUs.  "found" is the lowest list index
+Context.verify_blob): no per-candidate Python, one library context per stream over this client's GPUs kept
+across payloads (the library splits each payload over them).  "found" is the lowest list index
 that verifies (the reference reports whichever of its 4 racing workers exits first).
 """
 import argparse
@@ -30,12 +30,16 @@ HEARTBEAT_PORT = 31337
 HEARTBEAT_EVERY_S = 20
 
 
-def recvall(connection):
+def recvall(connection, deadline=None):
+    """Read until the peer half-closes.  deadline: time.time() limit; a peer still silent then raises
+    socket.timeout (a socket with a timeout but no deadline keeps waiting, as the reference does)."""
     chunks = []
     while True:
         try:
             chunk = connection.recv(1 << 20)
         except socket.timeout:
+            if deadline is not None and time.time() >= deadline:
+                raise
             continue
         if not chunk:
             return b"".join(chunks)
@@ -53,60 +57,66 @@ def prepare_message(identifier, found, password, hearthbeat=False):
 
 
 class GpuVerifier:
-    """Verifies payloads on this client's GPUs; contexts are created once per verifier stream."""
+    """Verifies payloads on this client's GPUs through one library context over all of them (the library
+    splits each payload into chunks over the devices); the context is created once per verifier stream."""
 
     def __init__(self, devices=None):
         if devices is None:
-            n = _lib.device_count()
-            if n < 1:
+            devices = _lib.device_list()
+            if not devices:
                 raise _lib.DprfError(_lib.E_NODEVICE, "no gfx950 device visible")
-            devices = list(range(n))
         self.devices = list(devices)
         self.stream = None
-        self.ctxs = []
+        self.ctx = None
         self.verified = 0
+        self.skipped = 0
         self.gpu_s = 0.0
 
-    def _contexts(self, stream):
+    def _context(self, stream):
         if stream != self.stream:
-            for c in self.ctxs:
-                c.close()
-            fields = parse_verification_data(stream)
-            self.ctxs = [_lib.Context(fields, device=d) for d in self.devices]
+            self.close()
+            self.ctx = _lib.Context(parse_verification_data(stream), devices=self.devices)
             self.stream = stream
-        return self.ctxs
+        return self.ctx
 
     def __call__(self, stream, blob, offsets):
-        """(found, password) for one payload, found = the lowest list index that verifies."""
-        ctxs = self._contexts(stream)
+        """(found, password) for one payload, found = the lowest list index that verifies.  A payload with
+        candidates the format cannot take (NUL, empty or invalid-UTF-8 Office passwords, over 64 bytes) is
+        verified without them -- the reference fails such a candidate in its own verifier process and goes
+        on with the rest (brute_force.py:106-161) -- instead of failing the payload on every client."""
+        import numpy as np
+        ctx = self._context(stream)
         n = len(offsets) - 1
         t0 = time.time()
-        per = -(-n // len(ctxs)) if n else 0
-        res = [None] * len(ctxs)
-
-        def work(k):
-            lo, hi = min(k * per, n), min((k + 1) * per, n)
-            if hi > lo:
-                h, _, _ = ctxs[k].verify_blob(blob, offsets[lo:hi + 1], stop_on_first=True, cap=1)
-                res[k] = lo + h[0] if h else None
-
-        if len(ctxs) == 1:
-            work(0)
-        else:
-            ths = [threading.Thread(target=work, args=(k,)) for k in range(len(ctxs))]
-            [t.start() for t in ths]
-            [t.join() for t in ths]
+        try:
+            h, _, _ = ctx.verify_blob(blob, offsets, stop_on_first=True, cap=1)
+            idx = h[0] if h else None
+        except _lib.DprfError as e:
+            if e.code not in (_lib.E_INVALID, _lib.E_DOMAIN, _lib.E_PWLEN):
+                raise
+            offs = np.asarray(offsets, dtype=np.uint64)
+            keep = np.flatnonzero(ctx.list_status(blob, offs) == 0)
+            self.skipped += n - len(keep)
+            print("Skipping %d candidate(s) the verifier cannot take (%s)" % (n - len(keep), e), flush=True)
+            idx = None
+            if len(keep):
+                buf = np.frombuffer(bytes(blob), dtype=np.uint8)
+                parts = [buf[int(offs[k]):int(offs[k + 1])] for k in keep]
+                sub = np.concatenate([np.zeros(1, np.uint64), np.cumsum([len(p) for p in parts], dtype=np.uint64)])
+                h, _, _ = ctx.verify_blob(np.concatenate(parts).tobytes() if parts else b"", sub,
+                                          stop_on_first=True, cap=1)
+                idx = int(keep[h[0]]) if h else None
         self.gpu_s += time.time() - t0
         self.verified += n
-        hits = [r for r in res if r is not None]
-        if hits:
-            return 1, candidate(blob, offsets, min(hits))
+        if idx is not None:
+            return 1, candidate(blob, offsets, idx)
         return 0, None
 
     def close(self):
-        for c in self.ctxs:
-            c.close()
-        self.ctxs = []
+        if self.ctx is not None:
+            self.ctx.close()
+        self.ctx = None
+        self.stream = None
 
 
 class DryRun:
@@ -171,8 +181,10 @@ def hearthbeat(tcp_ip, identifier, port=HEARTBEAT_PORT, every=HEARTBEAT_EVERY_S,
             client = socket.create_connection((tcp_ip, port), timeout=10)
             client.sendall(prepare_message(identifier, None, None, True))
             client.shutdown(socket.SHUT_WR)
-            recvall(client)
-            client.close()
+            try:
+                recvall(client, deadline=time.time() + 10)   # socket.timeout is an OSError: a failed beat
+            finally:
+                client.close()
         except OSError:
             print("Hearthbeat failed. Server seems to be down.", flush=True)
             return

@@ -3,13 +3,16 @@
  *
  * Replaces, per candidate batch, what brute_force.py does per candidate: the argv mapping
  * (_call_*_core, brute_force.py:163-197) becomes one context created from the field array; the
- * JoinableQueue + Popen + wait() loop (:106-161) becomes chunked kernel launches.  No verification
+ * JoinableQueue + Popen + wait() loop (:106-161) becomes chunked kernel launches, and the 4 worker
+ * processes on one queue (:70-73, :92-95) become one worker thread + HIP stream per GPU of the context on
+ * one shared chunk cursor.  No verification
  * runs on the host: a context whose reference verdict is constant (DPRF_FLAG_NEVER_MATCHES) is the
  * only case that launches nothing.
  */
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -17,6 +20,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dprf.h"
@@ -158,22 +162,38 @@ static const uint8_t PDF_PAD[32] = {0x28, 0xBF, 0x4E, 0x5E, 0x4E, 0x75, 0x8A, 0x
 /* ------------------------------------------------------------------ context */
 enum kernel_kind { K_NONE, K_OFFICE, K_ODT, K_PDF_R24, K_PDF_R5, K_PDF_R6 };
 static const uint32_t DEV_HIT_CAP = 1u << 20;
+static const int DEPTH = 3;   /* launches in flight per device before its worker retires the oldest */
 
-struct dprf_ctx {
-    int fmt = 0, flags = 0, device = 0;
-    kernel_kind kind = K_NONE;
+/* One device of a context: its stream, its copies of the tables and document constants, its result
+ * buffer, and a pinned ring of launch headers the worker thread reads instead of synchronising the stream
+ * (a stream sync would drain the launches queued behind the one being polled). */
+struct dev_lane {
+    int device = 0;
     hipStream_t stream = nullptr;
-    dprf_office_params office{};
-    dprf_odt_params odt{};
-    dprf_pdf_params pdf{};
     dprf_aes_tables *d_tables = nullptr;
     uint32_t *d_enc = nullptr;
     dprf_results *d_res = nullptr;
-    uint32_t *d_slots = nullptr;
     uint32_t *d_keys = nullptr;      /* KDF -> check hand-off, 8 words per candidate of one chunk */
+    uint32_t *d_slots = nullptr;     /* list mode: [n][DPRF_SLOT_WORDS] */
     uint8_t *d_lens = nullptr;
     size_t slot_cap = 0;
-    dprf_results *h_hdr = nullptr;   /* pinned copy of the results header */
+    dprf_results *h_ring = nullptr;  /* DEPTH launch headers + 1 (reset template / final header), pinned */
+    hipEvent_t ev[DEPTH][4] = {};    /* per ring slot: start, mid (KDF done), end, header copied */
+    dprf_odt_params odt{};           /* .enc -> this device's ciphertext copy */
+    double rate = 0;                 /* candidates per ms on this device (last full launch), 0 = unknown */
+};
+
+struct dprf_ctx {
+    int fmt = 0, flags = 0;
+    kernel_kind kind = K_NONE;
+    dprf_office_params office{};
+    dprf_odt_params odt{};
+    dprf_pdf_params pdf{};
+    std::vector<uint32_t> odt_words;  /* first min(len,1024) ciphertext bytes, BE words */
+    std::vector<dev_lane> lanes;
+    uint8_t *h_slots = nullptr;       /* list-mode staging (pinned, portable), shared by the lanes */
+    uint8_t *h_lens = nullptr;
+    size_t h_cap = 0;
 };
 
 static const char *kind_name(kernel_kind k) {
@@ -231,12 +251,9 @@ static int parse_odt(dprf_ctx *c, const char *const *f) {
     for (int i = 0; i < 4; i++) c->odt.salt[i] = be_word(&salt[4 * i]);
     c->odt.enc_len = (uint32_t)enc_len;
     c->odt.hash_len = (uint32_t)std::min(enc_len, 1024);
-    uint32_t nw = std::max<uint32_t>(4u, c->odt.hash_len / 4);
-    std::vector<uint32_t> words(nw, 0u);
-    for (uint32_t i = 0; i < c->odt.hash_len / 4; i++) words[i] = be_word(&enc[4 * i]);
-    HIPCHK(hipMalloc(&c->d_enc, nw * sizeof(uint32_t)));
-    HIPCHK(hipMemcpy(c->d_enc, words.data(), nw * sizeof(uint32_t), hipMemcpyHostToDevice));
-    c->odt.enc = c->d_enc;
+    const uint32_t nw = std::max<uint32_t>(4u, c->odt.hash_len / 4);
+    c->odt_words.assign(nw, 0u);
+    for (uint32_t i = 0; i < c->odt.hash_len / 4; i++) c->odt_words[i] = be_word(&enc[4 * i]);
     c->kind = K_ODT;
     return DPRF_OK;
 }
@@ -299,16 +316,29 @@ static int parse_pdf(dprf_ctx *c, const char *const *f) {
     return DPRF_OK;
 }
 
-/* candidates per launch, sized for ~0.05-0.2 s of device time per launch at the measured rates */
-static uint32_t chunk_for(kernel_kind k) {
+/* Candidates per launch.  A device takes its next chunk from the call's shared cursor sized for about
+ * `target_ms` of device time at the rate it measured on its last launch (`init` before the first), a
+ * power of two in [lo, hi].  The floors keep whole waves of workgroups on the chip: Office's 2^19 is one
+ * full generation of k_office_kdf (256 CUs x 32 waves x 64 lanes); R6's persistent workgroups need ~8
+ * candidates per slot per launch to amortise the round-length tail. */
+struct chunk_policy { uint32_t init, lo, hi; double target_ms; };
+static chunk_policy policy(kernel_kind k) {
     switch (k) {
-        case K_OFFICE: return 1u << 19;
-        case K_ODT: return 1u << 22;
-        case K_PDF_R24: return 1u << 24;
-        case K_PDF_R5: return 1u << 27;
-        case K_PDF_R6: return 1u << 21;
-        default: return 1u << 24;
+        case K_OFFICE: return {1u << 19, 1u << 19, 1u << 20, 400.0};
+        case K_ODT: return {1u << 22, 1u << 19, 1u << 23, 300.0};
+        case K_PDF_R24: return {1u << 24, 1u << 20, 1u << 30, 100.0};
+        case K_PDF_R5: return {1u << 27, 1u << 22, 1u << 31, 100.0};
+        case K_PDF_R6: return {1u << 21, 1u << 20, 1u << 22, 1000.0};
+        default: return {1u << 24, 1u << 20, 1u << 24, 100.0};
     }
+}
+static uint32_t lane_chunk(const dev_lane &L, kernel_kind k) {
+    const chunk_policy p = policy(k);
+    if (L.rate <= 0) return p.init;
+    const double want = L.rate * p.target_ms;
+    uint32_t c = p.lo;
+    while (c < p.hi && 2.0 * c <= want) c <<= 1;
+    return c;
 }
 
 /* ------------------------------------------------------------------ ABI: library */
@@ -320,80 +350,127 @@ static bool is_gfx950(int dev) {
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
     return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
-extern "C" int dprf_device_count(void) {
+extern "C" int dprf_device_list(int *ordinals, int cap) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     int k = 0;
-    for (int i = 0; i < n; i++) k += is_gfx950(i) ? 1 : 0;
+    for (int i = 0; i < n; i++)
+        if (is_gfx950(i)) {
+            if (ordinals && k < cap) ordinals[k] = i;
+            k++;
+        }
     return k;
 }
+extern "C" int dprf_device_count(void) { return dprf_device_list(nullptr, 0); }
 
 /* ------------------------------------------------------------------ ABI: context */
+static void lane_free(dev_lane &L) {
+    if (hipSetDevice(L.device) != hipSuccess) return;
+    if (L.stream) (void)hipStreamSynchronize(L.stream);
+    (void)hipFree(L.d_tables);
+    (void)hipFree(L.d_enc);
+    (void)hipFree(L.d_res);
+    (void)hipFree(L.d_slots);
+    (void)hipFree(L.d_lens);
+    (void)hipFree(L.d_keys);
+    if (L.h_ring) (void)hipHostFree(L.h_ring);
+    for (auto &s : L.ev)
+        for (auto &e : s)
+            if (e) (void)hipEventDestroy(e);
+    if (L.stream) (void)hipStreamDestroy(L.stream);
+    L = dev_lane();
+}
+
 extern "C" int dprf_ctx_destroy(dprf_ctx *c) {
     if (!c) return DPRF_OK;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->d_tables);
-    (void)hipFree(c->d_enc);
-    (void)hipFree(c->d_res);
-    (void)hipFree(c->d_slots);
-    (void)hipFree(c->d_lens);
-    (void)hipFree(c->d_keys);
-    if (c->h_hdr) (void)hipHostFree(c->h_hdr);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (auto &L : c->lanes) lane_free(L);
+    if (c->h_slots) (void)hipHostFree(c->h_slots);
+    if (c->h_lens) (void)hipHostFree(c->h_lens);
     delete c;
     return DPRF_OK;
 }
 
-extern "C" int dprf_ctx_create(const char *const *fields, int nfields, int device, dprf_ctx **out) {
-    if (!out || !fields || nfields < 1) return fail(DPRF_E_INVALID, "dprf_ctx_create: null argument");
+static int lane_init(dprf_ctx *c, dev_lane &L, int device) {
+    L.device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&L.d_tables, sizeof(dprf_aes_tables)));
+    HIPCHK(hipMemcpy(L.d_tables, &aes_tables(), sizeof(dprf_aes_tables), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&L.d_res, sizeof(dprf_results) + sizeof(unsigned long long) * DEV_HIT_CAP));
+    HIPCHK(hipHostMalloc(&L.h_ring, sizeof(dprf_results) * (DEPTH + 1), hipHostMallocDefault));
+    for (auto &s : L.ev)
+        for (auto &e : s) HIPCHK(hipEventCreate(&e));
+    if (c->kind == K_OFFICE || c->kind == K_ODT)
+        HIPCHK(hipMalloc(&L.d_keys, (size_t)8 * sizeof(uint32_t) * policy(c->kind).hi));
+    if (c->kind == K_ODT) {
+        HIPCHK(hipMalloc(&L.d_enc, c->odt_words.size() * sizeof(uint32_t)));
+        HIPCHK(hipMemcpy(L.d_enc, c->odt_words.data(), c->odt_words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        L.odt = c->odt;
+        L.odt.enc = L.d_enc;
+    }
+    return DPRF_OK;
+}
+
+extern "C" int dprf_ctx_create_devices(const char *const *fields, int nfields, const int *devices, int ndev,
+                                       dprf_ctx **out) {
+    if (!out || !fields || nfields < 1 || !devices || ndev < 1 || ndev > DPRF_MAX_DEVICES)
+        return fail(DPRF_E_INVALID, "dprf_ctx_create: null argument or device count %d", ndev);
     *out = nullptr;
     for (int i = 0; i < nfields; i++)
         if (!fields[i]) return fail(DPRF_E_INVALID, "dprf_ctx_create: field %d is NULL", i);
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || !is_gfx950(device))
-        return fail(DPRF_E_NODEVICE, "no gfx950 device with ordinal %d (%d HIP devices visible)", device, ndev);
+    int nhip = 0;
+    if (hipGetDeviceCount(&nhip) != hipSuccess) nhip = 0;
+    for (int k = 0; k < ndev; k++)
+        if (devices[k] < 0 || devices[k] >= nhip || !is_gfx950(devices[k]))
+            return fail(DPRF_E_NODEVICE, "no gfx950 device with ordinal %d (%d HIP devices visible)", devices[k], nhip);
     dprf_ctx *c = new dprf_ctx();
-    c->device = device;
     int r = DPRF_OK;
     const char *tag = fields[0];
-    if (hipSetDevice(device) != hipSuccess) { delete c; return fail(DPRF_E_HIP, "hipSetDevice(%d) failed", device); }
     /* parse_verification_data's accepted shapes (brute_force.py:253-260) */
     if (!strcmp(tag, "office") && nfields == 8) { c->fmt = DPRF_FMT_OFFICE; r = parse_office(c, fields); }
     else if (!strcmp(tag, "odt") && nfields == 7) { c->fmt = DPRF_FMT_ODT; r = parse_odt(c, fields); }
     else if (!strcmp(tag, "pdf") && nfields == 12) { c->fmt = DPRF_FMT_PDF; r = parse_pdf(c, fields); }
     else r = fail(DPRF_E_INVALID, "The input data is not supported (tag '%s', %d fields).", tag, nfields);
-    if (r != DPRF_OK) { std::string keep = g_err; dprf_ctx_destroy(c); g_err = keep; return r; }
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipMalloc(&c->d_tables, sizeof(dprf_aes_tables))) != hipSuccess ||
-        (e = hipMemcpy(c->d_tables, &aes_tables(), sizeof(dprf_aes_tables), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMalloc(&c->d_res, sizeof(dprf_results) + sizeof(unsigned long long) * DEV_HIT_CAP)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_hdr, sizeof(dprf_results), hipHostMallocDefault)) != hipSuccess) {
+    c->lanes.resize((size_t)ndev);
+    for (int k = 0; r == DPRF_OK && k < ndev; k++) r = lane_init(c, c->lanes[k], devices[k]);
+    if (r != DPRF_OK) {
+        std::string keep = g_err;
         dprf_ctx_destroy(c);
-        return fail(DPRF_E_HIP, "context allocation: %s", hipGetErrorString(e));
-    }
-    if (c->kind == K_OFFICE || c->kind == K_ODT) {
-        if ((e = hipMalloc(&c->d_keys, (size_t)8 * sizeof(uint32_t) * chunk_for(c->kind))) != hipSuccess) {
-            dprf_ctx_destroy(c);
-            return fail(DPRF_E_HIP, "key hand-off buffer: %s", hipGetErrorString(e));
-        }
+        g_err = keep;
+        return r;
     }
     *out = c;
     return DPRF_OK;
 }
+
+extern "C" int dprf_ctx_create(const char *const *fields, int nfields, int device, dprf_ctx **out) {
+    if (device == DPRF_ALL_DEVICES) {
+        int ords[DPRF_MAX_DEVICES];
+        const int n = std::min(dprf_device_list(ords, DPRF_MAX_DEVICES), DPRF_MAX_DEVICES);
+        if (n < 1) return fail(DPRF_E_NODEVICE, "no gfx950 device visible");
+        return dprf_ctx_create_devices(fields, nfields, ords, n, out);
+    }
+    return dprf_ctx_create_devices(fields, nfields, &device, 1, out);
+}
 extern "C" int dprf_ctx_format(const dprf_ctx *c) { return c ? c->fmt : DPRF_E_INVALID; }
 extern "C" int dprf_ctx_flags(const dprf_ctx *c) { return c ? c->flags : DPRF_E_INVALID; }
 extern "C" const char *dprf_ctx_kernel(const dprf_ctx *c) { return c ? kind_name(c->kind) : "none"; }
+extern "C" int dprf_ctx_devices(const dprf_ctx *c, int *ordinals, int cap) {
+    if (!c) return fail(DPRF_E_INVALID, "dprf_ctx_devices: null context");
+    for (int k = 0; k < (int)c->lanes.size() && k < cap; k++)
+        if (ordinals) ordinals[k] = c->lanes[k].device;
+    return (int)c->lanes.size();
+}
 
 /* ------------------------------------------------------------------ launching */
-static hipError_t launch(dprf_ctx *c, const dprf_enum &e, uint32_t cap, uint32_t stop, hipEvent_t mid) {
+static hipError_t launch(dprf_ctx *c, dev_lane &L, const dprf_enum &e, uint32_t stop, hipEvent_t mid) {
+    const uint32_t cap = DEV_HIT_CAP;
     switch (c->kind) {
-        case K_OFFICE: return launch_office(e, c->office, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys, mid);
-        case K_ODT: return launch_odt(e, c->odt, c->d_tables, c->d_res, cap, stop, c->stream, c->d_keys, mid);
-        case K_PDF_R24: return launch_pdf_r24(e, c->pdf, c->d_res, cap, stop, c->stream);
-        case K_PDF_R5: return launch_pdf_r5(e, c->pdf, c->d_res, cap, stop, c->stream);
-        case K_PDF_R6: return launch_pdf_r6(e, c->pdf, c->d_tables, c->d_res, cap, stop, c->stream);
+        case K_OFFICE: return launch_office(e, c->office, L.d_tables, L.d_res, cap, stop, L.stream, L.d_keys, mid);
+        case K_ODT: return launch_odt(e, L.odt, L.d_tables, L.d_res, cap, stop, L.stream, L.d_keys, mid);
+        case K_PDF_R24: return launch_pdf_r24(e, c->pdf, L.d_res, cap, stop, L.stream);
+        case K_PDF_R5: return launch_pdf_r5(e, c->pdf, L.d_res, cap, stop, L.stream);
+        case K_PDF_R6: return launch_pdf_r6(e, c->pdf, L.d_tables, L.d_res, cap, stop, L.stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -407,107 +484,173 @@ static void fastdiv_magic(uint32_t d, uint32_t &m, uint32_t &s) {
     s = l - 1;
 }
 
-struct run_state {
-    struct timing { hipEvent_t a, mid, b; };   /* mid: between KDF and check kernel (Office/ODF), else null */
-    std::vector<timing> ev;
-    std::chrono::steady_clock::time_point t0;
+/* State of one API call shared by its device workers. */
+struct call_state {
+    uint64_t total = 0;                  /* candidates of the call                                   */
+    uint64_t base = 0;                   /* index of offset 0 (range: start; list: 0)               */
+    int stop_on_first = 0;
+    std::atomic<uint64_t> next{0};       /* shared chunk cursor (offsets handed out in increasing order) */
+    std::atomic<uint64_t> first{~0ull};  /* lowest hit index any device has reported so far          */
+    std::atomic<int> err{0};
+    std::mutex mu;
+    std::string msg;
+    void error(int code, const std::string &m) {
+        int z = 0;
+        if (err.compare_exchange_strong(z, code)) {
+            std::lock_guard<std::mutex> g(mu);
+            msg = m;
+        }
+    }
+};
+static void atomic_min_u64(std::atomic<uint64_t> &a, uint64_t v) {
+    uint64_t cur = a.load();
+    while (v < cur && !a.compare_exchange_weak(cur, v)) {}
+}
+
+struct lane_result {
+    std::vector<unsigned long long> hits;
+    uint32_t nhits = 0;
+    uint64_t first = ~0ull, evaluated = 0, launches = 0;
+    double kms = 0, mms = 0;
 };
 
-static int reset_results(dprf_ctx *c) {
-    dprf_results h;
-    memset(&h, 0, sizeof h);
-    h.first = ~0ull;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(c->d_res, &h, sizeof(dprf_results), hipMemcpyHostToDevice));
-    return DPRF_OK;
-}
-
-/* Issue launches for [0, total) in chunks; mk(off, n) fills the dprf_enum for one chunk. */
+/* The worker of one device: take the next chunk from the shared cursor, launch it, keep DEPTH launches in
+ * flight, retire the oldest (timing, its header's lowest hit -> the call's `first`); with stop_on_first stop
+ * taking chunks once the next one starts above `first`.  Finally read this device's hits. */
 template <class MK>
-static int run_chunks(dprf_ctx *c, uint64_t total, int stop_on_first, uint32_t cap, MK mk, run_state &rs,
-                      int &stopped) {
-    const uint32_t chunk = chunk_for(c->kind);
-    const int depth = 3;   /* launches in flight before the host looks at the stop flag */
-    std::vector<hipEvent_t> poll;
-    stopped = 0;
-    uint64_t off = 0;
-    while (off < total) {
-        const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, total - off);
-        dprf_enum e;
-        memset(&e, 0, sizeof e);
-        mk(e, off, n);
-        hipEvent_t a, b, mid = nullptr;
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
-        if (c->kind == K_OFFICE || c->kind == K_ODT) HIPCHK(hipEventCreate(&mid));
-        HIPCHK(hipEventRecord(a, c->stream));
-        hipError_t le = launch(c, e, cap, stop_on_first ? 1u : 0u, mid);
-        if (le != hipSuccess) return fail(DPRF_E_HIP, "kernel launch (%s): %s", kind_name(c->kind), hipGetErrorString(le));
-        HIPCHK(hipEventRecord(b, c->stream));
-        rs.ev.push_back({a, mid, b});
-        off += n;
-        if (stop_on_first && off < total) {
-            poll.push_back(b);
-            if ((int)poll.size() >= depth) {
-                HIPCHK(hipEventSynchronize(poll[poll.size() - depth]));
-                HIPCHK(hipMemcpyAsync(c->h_hdr, c->d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, c->stream));
-                HIPCHK(hipStreamSynchronize(c->stream));
-                if (c->h_hdr->stop) { stopped = 1; break; }
-            }
+static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_result &out) {
+    char buf[600];
+    auto hip_fail = [&](const char *what, hipError_t e) {
+        snprintf(buf, sizeof buf, "%s (device %d): %s", what, L.device, hipGetErrorString(e));
+        cs.error(DPRF_E_HIP, buf);
+    };
+    hipError_t e = hipSetDevice(L.device);
+    if (e != hipSuccess) { hip_fail("hipSetDevice", e); return; }
+    dprf_results *fin = L.h_ring + DEPTH;
+    memset(fin, 0, sizeof *fin);
+    fin->first = ~0ull;
+    e = hipMemcpyAsync(L.d_res, fin, sizeof(dprf_results), hipMemcpyHostToDevice, L.stream);
+    if (e != hipSuccess) { hip_fail("reset results", e); return; }
+    const bool two = c->kind == K_OFFICE || c->kind == K_ODT;
+    uint32_t nchunk[DEPTH] = {};
+    int head = 0, inq = 0;
+    auto retire = [&]() -> hipError_t {
+        const int s = head;
+        hipError_t r = hipEventSynchronize(L.ev[s][3]);
+        if (r != hipSuccess) return r;
+        float ms = 0, m = 0;
+        (void)hipEventElapsedTime(&ms, L.ev[s][0], L.ev[s][2]);
+        if (two) (void)hipEventElapsedTime(&m, L.ev[s][0], L.ev[s][1]);
+        else m = ms;
+        out.kms += ms;
+        out.mms += m;
+        out.launches++;
+        const unsigned long long f = L.h_ring[s].first;
+        if (f != ~0ull) atomic_min_u64(cs.first, f);
+        else if (ms > 0.05f) L.rate = nchunk[s] / (double)ms;   /* a launch with no skipped blocks */
+        head = (head + 1) % DEPTH;
+        inq--;
+        return hipSuccess;
+    };
+    const char *failed = nullptr;
+    while (cs.err.load() == 0) {
+        const uint32_t want = lane_chunk(L, c->kind);
+        const uint64_t off = cs.next.fetch_add(want);
+        if (off >= cs.total) break;
+        if (cs.stop_on_first && cs.base + off > cs.first.load()) break;
+        if (inq == DEPTH) {
+            if ((e = retire()) != hipSuccess) { failed = "hipEventSynchronize"; break; }
+            if (cs.stop_on_first && cs.base + off > cs.first.load()) break;
         }
+        const uint32_t n = (uint32_t)std::min<uint64_t>(want, cs.total - off);
+        const int s = (head + inq) % DEPTH;
+        dprf_enum en;
+        memset(&en, 0, sizeof en);
+        if ((e = mk(L, en, off, n)) != hipSuccess) { failed = "candidate upload"; break; }
+        if ((e = hipEventRecord(L.ev[s][0], L.stream)) != hipSuccess) { failed = "hipEventRecord"; break; }
+        if ((e = launch(c, L, en, cs.stop_on_first ? 1u : 0u, two ? L.ev[s][1] : nullptr)) != hipSuccess) {
+            snprintf(buf, sizeof buf, "kernel launch (%s)", kind_name(c->kind));
+            hip_fail(buf, e);
+            break;
+        }
+        if ((e = hipEventRecord(L.ev[s][2], L.stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(&L.h_ring[s], L.d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, L.stream)) != hipSuccess ||
+            (e = hipEventRecord(L.ev[s][3], L.stream)) != hipSuccess) { failed = "launch bookkeeping"; break; }
+        nchunk[s] = n;
+        inq++;
     }
-    return DPRF_OK;
+    while (inq > 0) {
+        hipError_t r = retire();
+        if (r != hipSuccess) { if (!failed) { failed = "hipEventSynchronize"; e = r; } break; }
+    }
+    if (failed) { hip_fail(failed, e); return; }
+    if ((e = hipMemcpyAsync(fin, L.d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, L.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(L.stream)) != hipSuccess) { hip_fail("result header", e); return; }
+    out.nhits = fin->nhits;
+    out.first = fin->first;
+    out.evaluated = fin->evaluated;
+    const uint32_t ncopy = std::min<uint32_t>(out.nhits, DEV_HIT_CAP);
+    out.hits.resize(ncopy);
+    if (ncopy &&
+        (e = hipMemcpy(out.hits.data(), (char *)L.d_res + offsetof(dprf_results, hits),
+                       ncopy * sizeof(unsigned long long), hipMemcpyDeviceToHost)) != hipSuccess) {
+        hip_fail("hit list", e);
+        return;
+    }
+    std::sort(out.hits.begin(), out.hits.end());
+    if (out.nhits > DEV_HIT_CAP && out.first != ~0ull && out.hits[0] != out.first) {
+        /* the device buffer overflowed: keep the lowest hit */
+        out.hits.insert(out.hits.begin(), out.first);
+        out.hits.pop_back();
+    }
 }
 
-static int finish(dprf_ctx *c, run_state &rs, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats,
-                  int stopped) {
-    HIPCHK(hipMemcpyAsync(c->h_hdr, c->d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const uint32_t nh = c->h_hdr->nhits;
-    const uint32_t ncopy = std::min<uint32_t>(nh, DEV_HIT_CAP);
-    std::vector<unsigned long long> hv(ncopy);
-    if (ncopy)
-        HIPCHK(hipMemcpy(hv.data(), (char *)c->d_res + offsetof(dprf_results, hits), ncopy * sizeof(unsigned long long),
-                         hipMemcpyDeviceToHost));
-    std::sort(hv.begin(), hv.end());
-    if (nh > DEV_HIT_CAP && c->h_hdr->first != ~0ull && (hv.empty() || hv[0] != c->h_hdr->first)) {
-        /* overflowed the device buffer: make sure the lowest hit is reported first */
-        hv.insert(hv.begin(), c->h_hdr->first);
-        hv.pop_back();
-    }
-    if (hits)
-        for (int64_t i = 0; i < cap && i < (int64_t)hv.size(); i++) hits[i] = hv[i];
-    if (nhits) *nhits = nh;
+/* Run a call over every device of the context: one worker thread per device (the calling thread serves the
+ * first), then merge the devices' hits. */
+template <class MK>
+static int run_call(dprf_ctx *c, call_state &cs, MK mk, uint64_t *hits, int64_t cap, int64_t *nhits,
+                    dprf_stats *stats, std::chrono::steady_clock::time_point t0) {
+    const size_t nd = c->lanes.size();
+    std::vector<lane_result> res(nd);
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < nd; k++) th.emplace_back([&, k] { lane_run(c, c->lanes[k], cs, mk, res[k]); });
+    lane_run(c, c->lanes[0], cs, mk, res[0]);
+    for (auto &t : th) t.join();
+    if (cs.err.load() != 0) return fail(cs.err.load(), "%s", cs.msg.c_str());
+    std::vector<unsigned long long> all;
+    uint64_t nh = 0, evaluated = 0, launches = 0;
     double kms = 0, mms = 0;
-    for (auto &p : rs.ev) {
-        float ms = 0, m = 0;
-        (void)hipEventElapsedTime(&ms, p.a, p.b);
-        kms += ms;
-        if (p.mid) {
-            (void)hipEventElapsedTime(&m, p.a, p.mid);
-            mms += m;
-            (void)hipEventDestroy(p.mid);
-        } else {
-            mms += ms;
-        }
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
+    for (auto &r : res) {
+        all.insert(all.end(), r.hits.begin(), r.hits.end());
+        nh += r.nhits;
+        evaluated += r.evaluated;
+        launches += r.launches;
+        kms += r.kms;
+        mms += r.mms;
     }
+    std::sort(all.begin(), all.end());
+    if (hits)
+        for (int64_t i = 0; i < cap && i < (int64_t)all.size(); i++) hits[i] = all[i];
+    if (nhits) *nhits = (int64_t)nh;
     if (stats) {
-        stats->candidates = c->h_hdr->evaluated;
-        stats->launches = rs.ev.size();
+        stats->candidates = evaluated;
+        stats->launches = launches;
         stats->kernel_ms = kms;
         stats->main_kernel_ms = mms;
-        stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - rs.t0).count();
-        stats->stopped_early = (uint32_t)stopped;
+        stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->stopped_early = evaluated < cs.total ? 1u : 0u;
+        stats->devices = (uint32_t)nd;
     }
-    rs.ev.clear();
     return DPRF_OK;
 }
 
-static void empty_result(uint64_t count, int64_t *nhits, dprf_stats *stats) {
+static void empty_result(uint64_t count, int64_t *nhits, dprf_stats *stats, size_t nd) {
     if (nhits) *nhits = 0;
-    if (stats) { memset(stats, 0, sizeof *stats); stats->candidates = count; }
+    if (stats) {
+        memset(stats, 0, sizeof *stats);
+        stats->candidates = count;
+        stats->devices = (uint32_t)nd;
+    }
 }
 
 /* ------------------------------------------------------------------ ABI: range mode */
@@ -528,32 +671,30 @@ extern "C" int dprf_search_range(dprf_ctx *c, const uint8_t *charset, int cslen,
     if ((long double)start + (long double)count > space)
         return fail(DPRF_E_INVALID, "range [%llu, +%llu) exceeds the keyspace %d^%d", (unsigned long long)start,
                     (unsigned long long)count, cslen, pwlen);
-    if (hipSetDevice(c->device) != hipSuccess) return fail(DPRF_E_HIP, "hipSetDevice");
-    run_state rs;
-    rs.t0 = std::chrono::steady_clock::now();
-    if (c->kind == K_NONE || count == 0) { empty_result(count, nhits, stats); return DPRF_OK; }
-    int r = reset_results(c);
-    if (r) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (c->kind == K_NONE || count == 0) { empty_result(count, nhits, stats, c->lanes.size()); return DPRF_OK; }
     uint32_t m, s;
     fastdiv_magic((uint32_t)cslen, m, s);
-    const uint32_t cap_dev = DEV_HIT_CAP;
-    int stopped = 0;
-    r = run_chunks(c, count, stop_on_first, cap_dev,
-                   [&](dprf_enum &e, uint64_t off, uint32_t n) {
-                       e.start = start + off;
-                       e.count = n;
-                       e.mode = 0;
-                       e.pwlen = (uint32_t)pwlen;
-                       e.cslen = (uint32_t)cslen;
-                       e.div_m = m;
-                       e.div_s = s;
-                       uint64_t v = e.start;
-                       for (int p = pwlen - 1; p >= 0; p--) { e.sdig[p] = (uint8_t)(v % (uint64_t)cslen); v /= (uint64_t)cslen; }
-                       memcpy(e.charset, charset, (size_t)cslen);
-                   },
-                   rs, stopped);
-    if (r) return r;
-    return finish(c, rs, hits, cap, nhits, stats, stopped);
+    call_state cs;
+    cs.total = count;
+    cs.base = start;
+    cs.stop_on_first = stop_on_first;
+    return run_call(
+        c, cs,
+        [&](dev_lane &, dprf_enum &e, uint64_t off, uint32_t n) -> hipError_t {
+            e.start = start + off;
+            e.count = n;
+            e.mode = 0;
+            e.pwlen = (uint32_t)pwlen;
+            e.cslen = (uint32_t)cslen;
+            e.div_m = m;
+            e.div_s = s;
+            uint64_t v = e.start;
+            for (int p = pwlen - 1; p >= 0; p--) { e.sdig[p] = (uint8_t)(v % (uint64_t)cslen); v /= (uint64_t)cslen; }
+            memcpy(e.charset, charset, (size_t)cslen);
+            return hipSuccess;
+        },
+        hits, cap, nhits, stats, t0);
 }
 
 /* ------------------------------------------------------------------ ABI: list mode */
@@ -589,65 +730,104 @@ static int utf8_to_utf16le(const uint8_t *s, size_t n, uint8_t *out, size_t cap)
     return (int)o;
 }
 
+/* One candidate into its 64-byte slot, with the per-format conversion the reference's verifier applies
+ * before hashing: UTF-16LE (Office, iconv at msoffcrypto...c:80), 32-byte truncation (PDF R<=4,
+ * pdf...c:137), 127-byte truncation (PDF R5, :197-200).  Returns the slot's byte length or DPRF_E_*. */
+static int pack_candidate(const dprf_ctx *c, const uint8_t *pw, size_t len, uint8_t *dst) {
+    const size_t SB = DPRF_SLOT_WORDS * 4;
+    memset(dst, 0, SB);
+    if (memchr(pw, 0, len)) return DPRF_E_INVALID;              /* argv cannot carry a NUL */
+    if (c->fmt == DPRF_FMT_OFFICE) {
+        if (len == 0) return DPRF_E_DOMAIN;                     /* reference UB on the iconv path */
+        const int u = utf8_to_utf16le(pw, len, dst, SB);
+        if (u == -1) return DPRF_E_DOMAIN;                      /* iconv fails on invalid UTF-8 */
+        if (u < 0) return DPRF_E_PWLEN;
+        return u;
+    }
+    if (c->kind == K_PDF_R24 && len > 32) len = 32;
+    if (c->kind == K_PDF_R5 && len > 127) len = 127;
+    if (len > SB) return DPRF_E_PWLEN;
+    memcpy(dst, pw, len);
+    return (int)len;
+}
+static const char *status_text(int code) {
+    switch (code) {
+        case DPRF_E_INVALID: return "contains NUL (argv cannot carry it)";
+        case DPRF_E_DOMAIN: return "empty or invalid UTF-8 Office password (the reference's iconv path fails)";
+        case DPRF_E_PWLEN: return "longer than the kernels' 64-byte slot (32 UTF-16 code units for Office)";
+        default: return "invalid";
+    }
+}
+
+extern "C" int dprf_list_status(const dprf_ctx *c, const uint8_t *blob, const uint64_t *offsets, int64_t n,
+                                int8_t *status) {
+    if (!c || n < 0 || (n > 0 && (!blob || !offsets))) return fail(DPRF_E_INVALID, "dprf_list_status: bad argument");
+    uint8_t slot[DPRF_SLOT_WORDS * 4];
+    int64_t bad = 0;
+    for (int64_t k = 0; k < n; k++) {
+        int r = offsets[k + 1] < offsets[k] ? DPRF_E_INVALID
+                                            : pack_candidate(c, blob + offsets[k], (size_t)(offsets[k + 1] - offsets[k]), slot);
+        r = r < 0 ? r : 0;
+        if (status) status[k] = (int8_t)r;
+        bad += r < 0;
+    }
+    return (int)std::min<int64_t>(bad, INT32_MAX);
+}
+
 extern "C" int dprf_verify_list(dprf_ctx *c, const uint8_t *blob, const uint64_t *offsets, int64_t n,
                                 int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats) {
     if (!c || (n > 0 && (!blob || !offsets)) || n < 0) return fail(DPRF_E_INVALID, "dprf_verify_list: bad argument");
-    if (hipSetDevice(c->device) != hipSuccess) return fail(DPRF_E_HIP, "hipSetDevice");
-    run_state rs;
-    rs.t0 = std::chrono::steady_clock::now();
-    /* pack candidates into 64-byte slots, with the per-format input conversion the reference's
-     * verifier applies before hashing: UTF-16LE (Office), 32-byte truncation (PDF R<=4, pdf...c:137),
-     * 127-byte truncation (PDF R5, :197-200) */
+    const auto t0 = std::chrono::steady_clock::now();
     const size_t SB = DPRF_SLOT_WORDS * 4;
-    std::vector<uint8_t> slots((size_t)n * SB, 0), lens((size_t)n, 0);
+    if ((size_t)n > c->h_cap) {
+        const size_t want = std::max<size_t>((size_t)n, 2 * c->h_cap);
+        if (c->h_slots) (void)hipHostFree(c->h_slots);
+        if (c->h_lens) (void)hipHostFree(c->h_lens);
+        c->h_slots = nullptr;
+        c->h_lens = nullptr;
+        c->h_cap = 0;
+        HIPCHK(hipHostMalloc(&c->h_slots, want * SB, hipHostMallocPortable));
+        HIPCHK(hipHostMalloc(&c->h_lens, want, hipHostMallocPortable));
+        c->h_cap = want;
+    }
     for (int64_t k = 0; k < n; k++) {
         if (offsets[k + 1] < offsets[k]) return fail(DPRF_E_INVALID, "offsets not monotone at %lld", (long long)k);
-        const uint8_t *pw = blob + offsets[k];
-        size_t len = (size_t)(offsets[k + 1] - offsets[k]);
-        if (memchr(pw, 0, len)) return fail(DPRF_E_INVALID, "candidate %lld contains NUL (argv cannot carry it)", (long long)k);
-        uint8_t *dst = &slots[(size_t)k * SB];
-        if (c->fmt == DPRF_FMT_OFFICE) {
-            if (len == 0) return fail(DPRF_E_DOMAIN, "candidate %lld: empty Office password (reference UB, iconv path)", (long long)k);
-            int u = utf8_to_utf16le(pw, len, dst, SB);
-            if (u == -1) return fail(DPRF_E_DOMAIN, "candidate %lld: invalid UTF-8 (reference iconv fails)", (long long)k);
-            if (u < 0) return fail(DPRF_E_PWLEN, "candidate %lld: more than 32 UTF-16 code units", (long long)k);
-            lens[k] = (uint8_t)u;
-            continue;
-        }
-        if (c->kind == K_PDF_R24 && len > 32) len = 32;
-        if (c->kind == K_PDF_R5 && len > 127) len = 127;
-        if (len > SB) return fail(DPRF_E_PWLEN, "candidate %lld: %zu bytes > %zu", (long long)k, len, SB);
-        memcpy(dst, pw, len);
-        lens[k] = (uint8_t)len;
+        const int r = pack_candidate(c, blob + offsets[k], (size_t)(offsets[k + 1] - offsets[k]), c->h_slots + (size_t)k * SB);
+        if (r < 0) return fail(r, "candidate %lld: %s", (long long)k, status_text(r));
+        c->h_lens[k] = (uint8_t)r;
     }
-    if (c->kind == K_NONE || n == 0) { empty_result((uint64_t)n, nhits, stats); return DPRF_OK; }
-    if ((size_t)n > c->slot_cap) {
-        (void)hipFree(c->d_slots);
-        (void)hipFree(c->d_lens);
-        c->d_slots = nullptr;
-        c->d_lens = nullptr;
-        c->slot_cap = 0;
-        HIPCHK(hipMalloc(&c->d_slots, (size_t)n * SB));
-        HIPCHK(hipMalloc(&c->d_lens, (size_t)n));
-        c->slot_cap = (size_t)n;
-    }
-    HIPCHK(hipMemcpyAsync(c->d_slots, slots.data(), (size_t)n * SB, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_lens, lens.data(), (size_t)n, hipMemcpyHostToDevice, c->stream));
-    int r = reset_results(c);
-    if (r) return r;
-    int stopped = 0;
-    r = run_chunks(c, (uint64_t)n, stop_on_first, DEV_HIT_CAP,
-                   [&](dprf_enum &e, uint64_t off, uint32_t cnt) {
-                       e.start = off;
-                       e.count = cnt;
-                       e.mode = 1;
-                       e.pwlen = *std::max_element(lens.begin() + (ptrdiff_t)off, lens.begin() + (ptrdiff_t)(off + cnt));
-                       e.slots = c->d_slots;
-                       e.lens = c->d_lens;
-                   },
-                   rs, stopped);
-    if (r) return r;
-    /* the host vectors must outlive the async copies */
-    r = finish(c, rs, hits, cap, nhits, stats, stopped);
-    return r;
+    if (c->kind == K_NONE || n == 0) { empty_result((uint64_t)n, nhits, stats, c->lanes.size()); return DPRF_OK; }
+    call_state cs;
+    cs.total = (uint64_t)n;
+    cs.base = 0;
+    cs.stop_on_first = stop_on_first;
+    return run_call(
+        c, cs,
+        [&](dev_lane &L, dprf_enum &e, uint64_t off, uint32_t cnt) -> hipError_t {
+            hipError_t r;
+            if (L.slot_cap < (size_t)n) {   /* first chunk of the call on this device: nothing in flight */
+                (void)hipFree(L.d_slots);
+                (void)hipFree(L.d_lens);
+                L.d_slots = nullptr;
+                L.d_lens = nullptr;
+                L.slot_cap = 0;
+                if ((r = hipMalloc(&L.d_slots, (size_t)n * SB)) != hipSuccess) return r;
+                if ((r = hipMalloc(&L.d_lens, (size_t)n)) != hipSuccess) return r;
+                L.slot_cap = (size_t)n;
+            }
+            /* this chunk's slots only: a device uploads what it verifies */
+            if ((r = hipMemcpyAsync((uint8_t *)L.d_slots + off * SB, c->h_slots + off * SB, (size_t)cnt * SB,
+                                    hipMemcpyHostToDevice, L.stream)) != hipSuccess)
+                return r;
+            if ((r = hipMemcpyAsync(L.d_lens + off, c->h_lens + off, cnt, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
+                return r;
+            e.start = off;
+            e.count = cnt;
+            e.mode = 1;
+            e.pwlen = *std::max_element(c->h_lens + off, c->h_lens + off + cnt);
+            e.slots = L.d_slots;
+            e.lens = L.d_lens;
+            return hipSuccess;
+        },
+        hits, cap, nhits, stats, t0);
 }

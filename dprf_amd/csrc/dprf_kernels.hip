@@ -68,10 +68,14 @@ DEVI void get_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand 
 }
 
 /* ------------------------------------------------------------------ block prologue / epilogue */
-/* Stage the charset (and optionally the AES tables) into LDS, read the stop flag once per block. */
+/* Stage the charset (and optionally the AES tables) into LDS and decide once per block whether it runs.
+ * With stop_on_first a block is skipped only when its LOWEST candidate index lies above the lowest hit
+ * found so far (R->first): every index below the final `first` is then verified whatever order the
+ * workgroups are dispatched in, so the reported hit is the lowest of the call unconditionally (a boolean
+ * stop flag would let a late-dispatched lower block skip itself).  `per` = candidates per thread. */
 template <bool AES>
 DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_results *R, uint32_t stop_on_first,
-                         uint8_t *cs, aes_lds *L, uint32_t *flag) {
+                         uint8_t *cs, aes_lds *L, uint32_t *flag, uint32_t per = 1) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < 64; k += blockDim.x) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     if (AES) {
@@ -81,7 +85,14 @@ DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_resu
             L->isb[k] = ((const uint32_t *)T->inv_sbox)[k];
         }
     }
-    if (tid == 0) *flag = stop_on_first ? __hip_atomic_load(&R->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if (tid == 0) {
+        uint32_t skip = 0u;
+        if (stop_on_first) {
+            const unsigned long long base = e.start + (unsigned long long)blockIdx.x * blockDim.x * per;
+            skip = base > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+        }
+        *flag = skip;
+    }
     __syncthreads();
     return *flag == 0;
 }
@@ -443,7 +454,7 @@ __global__ void __launch_bounds__(256)
 k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
-    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
+    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag, R5_PER)) return;
     const uint32_t base = blockIdx.x * (blockDim.x * R5_PER);
     /* Range mode: every candidate has length pwlen <= DPRF_MAX_RANGE_LEN, so the message is one block and
      * its tail -- salt8 || 0x80 at byte pwlen, the bit length in word 15 -- is the same for the whole
@@ -792,7 +803,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     uint32_t *flag = (uint32_t *)(S + 256);
     uint32_t *padw = (uint32_t *)(S + 320);               /* PAD || PAD for the runtime-offset padding */
     if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
-    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag)) return;
+    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag, PER)) return;
     const uint32_t base = blockIdx.x * (64u * PER);
     const uint32_t lanebase = (threadIdx.x & 63u) << 2;
     /* range mode: PAD[0:32-pwlen] placed at byte pwlen (pdf...c:136-139), 8 LE words, launch-uniform */

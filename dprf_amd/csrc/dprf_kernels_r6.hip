@@ -27,6 +27,8 @@
 #include "dprf_params.h"
 #include "dprf_launch.h"
 
+#include <mutex>
+
 /* Te0 replicated 32x: entry x, copy c at byte 256*x + 4*c (c < 32).  Lane l reads copy l%32, so each
  * 32-lane group of a ds_read_b32 ({0-31}, {32-63}: MI355X_MICROARCH.md LDS table) hits 32 different banks
  * whatever the indices (conflict-free), and the address of byte k of a state word is ONE v_perm: byte 1
@@ -364,11 +366,13 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
 template <int MODE>
 DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, dprf_results *R,
                    uint32_t stop_on_first, r6_shared *sh, const r6_lds &S, uint32_t slot) {
-    uint32_t c = R6_IDLE;
-    if (!(stop_on_first && __hip_atomic_load(&R->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        c = atomicAdd(&R->cursor, 1u);
-        if (c >= e.count) c = R6_IDLE;
-    }
+    /* the cursor hands out candidates in increasing order, so every candidate below one that is taken has
+     * been taken and will finish: skipping those above the lowest hit so far (stop_on_first) keeps the
+     * reported hit the lowest of the call */
+    uint32_t c = atomicAdd(&R->cursor, 1u);
+    if (c >= e.count ||
+        (stop_on_first && e.start + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        c = R6_IDLE;
     sh->cand[slot] = c;
     if (c != R6_IDLE) {
         uint32_t K[16];
@@ -544,6 +548,10 @@ static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots
     *shm = 256 + (sizeof(r6_shared) + 15) / 16 * 16 + (size_t)(dyn / 64u) * pat_words * 256u;   /* + static r6_te */
 }
 
+#define R6_MAX_DEVICES 64
+static std::mutex r6_attr_mu;
+static bool r6_attr_set[2][R6_MAX_DEVICES];
+
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
     /* longest password of the launch (list mode: the host's maximum over the chunk): the period length
@@ -558,23 +566,32 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     /* lanes: 12 waves, or fewer when there are fewer slots */
     uint32_t lanes = (nslots / 64u) * 64u;
     if (lanes > R6_LANES) lanes = R6_LANES;
-    static bool attr_set[2] = {false, false};
     /* the work cursor restarts at 0 for every launch (stream-ordered before the kernel) */
     hipError_t me = hipMemsetAsync(&R->cursor, 0, sizeof(uint32_t), s);
     if (me != hipSuccess) return me;
     int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
+    if ((me = hipGetDevice(&dev)) != hipSuccess) return me;
+    if (dev < 0 || dev >= R6_MAX_DEVICES) return hipErrorInvalidDevice;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
     /* one workgroup per CU; a launch smaller than the slots it would open uses fewer workgroups */
     uint32_t grid = (e.count + nslots - 1) / nslots;
     if (grid > (uint32_t)ncu) grid = (uint32_t)ncu;
-    if (e.mode == 0) {
-        if (!attr_set[0]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[0] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
-    } else {
-        if (!attr_set[1]) { (void)hipFuncSetAttribute((const void *)k_pdf_r6<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES); attr_set[1] = true; }
-        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
+    const void *fn = e.mode == 0 ? (const void *)k_pdf_r6<0> : (const void *)k_pdf_r6<1>;
+    {
+        /* function attributes are per device: set once per (device, mode), under a lock -- the device
+         * workers of a multi-device context launch concurrently */
+        std::lock_guard<std::mutex> g(r6_attr_mu);
+        bool &done = r6_attr_set[e.mode == 0 ? 0 : 1][dev];
+        if (!done) {
+            me = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES);
+            if (me != hipSuccess) return me;
+            done = true;
+        }
     }
+    if (e.mode == 0)
+        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
+    else
+        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
     return hipGetLastError();
 }

@@ -33,6 +33,7 @@ from .payload import LOWERCASE, Keyspace, build_message
 HEARTBEAT_PORT = 31337
 INACTIVE_AFTER_S = 120          # server.py:52-53
 CLEANUP_EVERY_S = 120           # server.py:241-244
+REQUEST_TIMEOUT_S = 60          # a work request not finished in this time is dropped (reference: waits forever)
 
 
 class Client:
@@ -56,13 +57,16 @@ class Client:
         self.last_activity = last_activity
 
 
-def recvall(connection):
-    """Read until the peer half-closes (server.py:171-183)."""
+def recvall(connection, deadline=None):
+    """Read until the peer half-closes (server.py:171-183).  deadline: time.time() limit after which a peer
+    that is still silent raises socket.timeout (an OSError) instead of holding the thread forever."""
     chunks = []
     while True:
         try:
             chunk = connection.recv(1 << 16)
         except socket.timeout:
+            if deadline is not None and time.time() >= deadline:
+                raise
             continue
         if not chunk:
             return b"".join(chunks)
@@ -134,7 +138,8 @@ class Server:
         found = False
         self.log("A client connected from address:", address)
         try:
-            data = json.loads(recvall(client))
+            client.settimeout(REQUEST_TIMEOUT_S)
+            data = json.loads(recvall(client, deadline=time.time() + REQUEST_TIMEOUT_S))
             client.shutdown(socket.SHUT_RD)
             client_identifier = data["id"]
         except (OSError, ValueError, KeyError, TypeError):
@@ -158,7 +163,16 @@ class Server:
             self.correct_password = data.get("correct_password")
             found = True
         elif message:
-            client.sendall(message)
+            try:
+                client.sendall(message)
+            except OSError:
+                # the client died between its request and our answer: keep the payload for the next
+                # connection (the caller still holds message/segs) and forget a client that never got one
+                client.close()
+                if not known:
+                    with self.lock:
+                        self.clients = [c for c in self.clients if c.id != client_identifier]
+                return False, False
             if self.first_send is None:
                 self.first_send = time.time()
             with self.lock:
@@ -191,7 +205,7 @@ class Server:
                 break
             try:
                 client.settimeout(10)
-                data = json.loads(recvall(client))
+                data = json.loads(recvall(client, deadline=time.time() + 10))
                 with self.lock:
                     for c in self.clients:
                         if c.id == data.get("id"):

@@ -12,8 +12,12 @@
  * never reported as "found" (the reference conflates the two: any non-zero exit counts as a hit,
  * brute_force.py:140).
  *
- * Threading: a context is bound to one device and owns one HIP stream; calls on DIFFERENT contexts may
- * run concurrently from different threads; calls on the SAME context must be serialised by the caller.
+ * Threading: a context spans a list of devices (one or all of the node's GPUs) and owns one host worker
+ * thread and one HIP stream per device for the duration of a call: dprf_search_range / dprf_verify_list
+ * fan the call out over the devices inside the library (the reference's 4 worker processes on one queue,
+ * brute_force.py:70-73 / :92-95, become one worker thread per GPU on one shared chunk cursor).  Calls on
+ * DIFFERENT contexts may run concurrently from different threads; calls on the SAME context must be
+ * serialised by the caller.
  * Ownership: the caller owns every buffer it passes; they are read/written only during the call.
  */
 #ifndef DPRF_H
@@ -24,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 2
+#define DPRF_ABI_VERSION 3
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -40,6 +44,9 @@ extern "C" {
 #define DPRF_E_NODEVICE (-4)     /* no usable gfx950 device / bad device ordinal                  */
 #define DPRF_E_PWLEN (-5)        /* candidate longer than the kernel supports (see DPRF_MAX_PW)    */
 #define DPRF_E_CHARSET (-6)      /* charset invalid for this format (e.g. non-ASCII for Office)    */
+
+#define DPRF_ALL_DEVICES (-1)    /* dprf_ctx_create device argument: every gfx950 device visible    */
+#define DPRF_MAX_DEVICES 64
 
 /* context flags (dprf_ctx_flags) */
 #define DPRF_FLAG_NEVER_MATCHES 1        /* reference verify() returns 0 for every candidate: (V,R)
@@ -63,22 +70,31 @@ typedef struct dprf_stats {
     double kernel_ms;      /* sum of HIP-event durations of those launches (on the ctx stream)  */
     double wall_ms;        /* host wall time of the call, first launch to last result copy      */
     uint32_t stopped_early;/* 1 if stop_on_first ended the search before the whole range        */
-    uint32_t reserved;
+    uint32_t devices;      /* devices that took part in the call (ABI 3; was `reserved`)        */
     double main_kernel_ms; /* HIP-event time of the dominant kernel alone: the KDF kernel for Office/ODF
                               (their check kernel follows it on the same stream), else = kernel_ms  (ABI 2) */
 } dprf_stats;
+/* kernel_ms / main_kernel_ms are summed over the devices of a multi-device call (device time); wall_ms is
+ * the call's wall time.  candidates / launches are totals over the devices. */
 
 /* ---- library ---- */
 int dprf_abi_version(void);
 const char *dprf_last_error(void);
 int dprf_device_count(void);      /* gfx950 devices visible to this process */
+/* HIP ordinals of the visible gfx950 devices (a non-gfx950 device may sit at any ordinal): writes up to
+ * cap ordinals, returns how many there are (ABI 3) */
+int dprf_device_list(int *ordinals, int cap);
 
-/* ---- context: one document, one device ----
+/* ---- context: one document, one or more devices ----
  * fields/nfields: the array parse_verification_data() returns (brute_force.py:245-264), i.e. the
  * stream split on '*' with fields[0] replaced by the format tag ("office", "odt" or "pdf"); office
  * needs 8 fields, odt 7, pdf 12.  The per-format field meaning is exactly the reference's argv mapping
- * (brute_force.py:163-197).  device: HIP device ordinal. */
+ * (brute_force.py:163-197).  device: HIP device ordinal, or DPRF_ALL_DEVICES for every gfx950 device. */
 int dprf_ctx_create(const char *const *fields, int nfields, int device, dprf_ctx **out);
+/* The same over an explicit device list (ABI 3).  An ordinal may repeat: {0,0} runs two streams and two
+ * worker threads on device 0 (used to test the multi-device path on one GPU). */
+int dprf_ctx_create_devices(const char *const *fields, int nfields, const int *devices, int ndev, dprf_ctx **out);
+int dprf_ctx_devices(const dprf_ctx *ctx, int *ordinals, int cap);   /* returns the device count */
 int dprf_ctx_destroy(dprf_ctx *ctx);
 int dprf_ctx_format(const dprf_ctx *ctx);
 int dprf_ctx_flags(const dprf_ctx *ctx);
@@ -87,8 +103,13 @@ const char *dprf_ctx_kernel(const dprf_ctx *ctx);   /* kernel family name, e.g. 
 /* ---- range mode: brute_force.py -pr N (init_rangebased_brute_force :60-79, _generate :199-219) ----
  * Verifies candidates [start, start+count) of charset^pwlen in itertools.product order (leftmost
  * character most significant).  Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total
- * number of hits found (may exceed cap).  stop_on_first != 0 stops after the launch containing the
- * lowest hit, which is then hits[0].  stats may be NULL. */
+ * number of hits found (may exceed cap).  stats may be NULL.
+ * Multi-device: the devices take contiguous chunks of the range from one shared cursor in increasing
+ * order (chunks sized for ~0.1-1 s of device time at the rate measured on that device), so a fast device
+ * takes more and every index below the last chunk taken is covered.
+ * stop_on_first != 0: the search ends once no unverified index lies below the lowest hit found so far;
+ * hits[0] is then the LOWEST verifying index of the whole range, unconditionally (every candidate below
+ * it is verified on some device; a kernel block is skipped only if its lowest index is above it). */
 int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwlen, uint64_t start,
                       uint64_t count, int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits,
                       dprf_stats *stats);
@@ -97,6 +118,12 @@ int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwle
  * Candidate k is blob[offsets[k] .. offsets[k+1]) (n+1 offsets).  Hits are list indices. */
 int dprf_verify_list(dprf_ctx *ctx, const uint8_t *blob, const uint64_t *offsets, int64_t n,
                      int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats);
+/* dprf_verify_list rejects the whole call if one candidate is invalid for the format (NUL, empty or
+ * invalid-UTF-8 Office password, longer than DPRF_MAX_PW after truncation).  This host-only check (no
+ * device work) writes 0 or that DPRF_E_* code per candidate to status[n] (may be NULL) and returns the
+ * number of invalid candidates, so a caller can drop them and verify the rest -- the reference fails
+ * such a candidate alone, in its own verifier process (brute_force.py:163-197).  (ABI 3) */
+int dprf_list_status(const dprf_ctx *ctx, const uint8_t *blob, const uint64_t *offsets, int64_t n, int8_t *status);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,59 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+class OracleCtx:
+    """Stand-in for _lib.Context on CPU (test infrastructure): the oracle's verdicts over the same range."""
+
+    def __init__(self, stream):
+        import pyoracle
+        self.c = pyoracle.Ctx(stream)
+
+    def search_range(self, cs, pwlen, start, n, stop_on_first=False, cap=1 << 16):
+        hits, nh = self.c.search_range(cs, pwlen, start, n, nthreads=2)
+        return hits[:cap], nh, {"candidates": n, "wall_ms": 1.0, "launches": 1, "kernel_ms": 1.0,
+                                "main_kernel_ms": 1.0, "devices": 1}
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.run_workload itself on two gloo ranks with an oracle-backed context: the shards, the per-round
+    call (brute_force.search_round) and the MIN exchange of a REAL hit (PDF R5 doc, password 'cat')."""
+    import sys
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(here, "oracle"))
+    import json
+    import bench
+    streams = json.load(open(os.path.join(here, "tests", "golden", "streams.json")))
+    bench.WORKLOADS["test_r5"] = ("pdf_synth_r5_cat", bench.LOWER, 3, 1000, "pdf_r5", "gloo test")
+
+    def amin(v):
+        t = torch.tensor([v], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
+    ctx = OracleCtx(streams["pdf_synth_r5_cat"]["stream"])
+    dt, stats, lowest, pwlen = bench.run_workload("test_r5", ctx, rank, world, 3, 0, dist.barrier, amin)
+    q.put((rank, lowest, pwlen, [s["candidates"] for s in stats]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_run_workload_two_ranks_min_of_a_real_hit():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    [p.join(120) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    want = 2 * 676 + 0 * 26 + 19          # "cat" in lowercase^3 product order, verified by rank 1 in step 0
+    assert [r[1] for r in res] == [want, want]
+    assert all(r[2] == 3 and r[3] == [1000, 1000, 1000] for r in res)
+
+
 def test_two_rank_shards_and_allreduce():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
@@ -61,17 +114,14 @@ def test_two_rank_shards_and_allreduce():
     assert tmax == [1.5, 1.5]
 
 
-def test_brute_force_round_slices_tile_the_block():
-    """brute_force's in-process multi-device rounds: every device gets a contiguous slice of the round's
-    block and the slices tile it (the lowest hit of a round is then the lowest overall)."""
+def test_brute_force_rounds_are_sized_by_time():
+    """brute_force's range rounds: the first is FIRST_ROUND candidates, later ones ~ROUND_SECONDS at the
+    measured rate, never past the end of the keyspace (the library splits each round over the devices)."""
     from dprf_amd import brute_force as bf
-    for ndev in (1, 2, 3, 8):
-        for done, block in ((0, 1000), (5000, 7), (123, 1 << 20)):
-            sl = bf._round_slices(done, block, ndev)
-            assert sl[0][0] == done
-            for (a, n), (b, _) in zip(sl, sl[1:]):
-                assert a + n == b
-            assert sum(n for _, n in sl) == block
+    assert bf.next_round(0.0, 1 << 40) == bf.FIRST_ROUND
+    assert bf.next_round(1e9, 1 << 40) == int(1e9 * bf.ROUND_SECONDS)
+    assert bf.next_round(10.0, 1 << 40) == bf.FIRST_ROUND
+    assert bf.next_round(1e9, 12345) == 12345
 
 
 def test_small_keyspace_shards_stay_disjoint_at_eight_ranks():
@@ -85,9 +135,9 @@ def test_small_keyspace_shards_stay_disjoint_at_eight_ranks():
         def __init__(self, rank):
             self.rank = rank
 
-        def search_range(self, cs, pwlen, start, n):
+        def search_range(self, cs, pwlen, start, n, stop_on_first=False, cap=1 << 16):
             seen.setdefault(pwlen, []).append((start, n))
-            return [], 0, {"candidates": n}
+            return [], 0, {"candidates": n, "wall_ms": 1.0}
 
     world = 8
     for rank in range(world):

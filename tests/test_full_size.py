@@ -4,6 +4,11 @@ keyspace -- past 2^32 for the alnum^7 and lowercase^8 spaces (the u64 enumeratio
 and of the server's global order), or at its very last index -- is searched in range mode over a window
 around that index at the config's own charset and length.  The lowest hit must be the planted index, and
 every hit the GPU reports must verify on the oracle (the CPU restatement of the reference verifiers).
+
+Two-way at full size (TWO_WAY): for the formats the oracle scans fast enough -- PDF R2, R3/R4, R5 and the
+ODF `-e` stream (a 2-byte check, ~2^-16 false positives) -- a complete sub-window of >= 2^20 indices
+(2^15 for ODF -e) deep in the config's keyspace is scanned by both, and the GPU's hit set must EQUAL the
+oracle's: no false negative anywhere in the window, not only "the planted index is found".
 """
 import os
 import tempfile
@@ -23,6 +28,17 @@ CASES = [
     ("pdf-r2-alnum7", "pdf", {"R": 2, "length": 40}, ALNUM, "Mo3kV9b", 1 << 26),
     ("pdf-r5-alnum7-first", "pdf", {"R": 5, "length": 256}, ALNUM, "aaaaaaa", 1 << 26),
 ]
+
+
+# (config, writer kind, writer kwargs, charset, password, window): complete windows, oracle == GPU
+TWO_WAY = [
+    ("pdf-r2-alnum7", "pdf", {"R": 2, "length": 40}, ALNUM, "Mo3kV9b", 1 << 22),
+    ("configs2-pdf-r4-alnum7", "pdf", {"R": 4, "length": 128}, ALNUM, "q7ZpL02", 1 << 20),
+    ("configs2-pdf-r3-alnum7-last", "pdf", {"R": 3, "length": 128}, ALNUM, "9999999", 1 << 20),
+    ("pdf-r5-alnum7-deep", "pdf", {"R": 5, "length": 256}, ALNUM, "Kq3Zr8w", 1 << 24),
+    ("configs1-odt-e-alnum6", "odt_e", {}, ALNUM, "Zx9Qa7", 1 << 15),
+]
+ORACLE_THREADS = 16      # the GPU box's CPU share
 
 
 def index_of(pw, cs):
@@ -48,9 +64,10 @@ def _doc_streams(t, kind, kw, pw, seed):
     if kind == "docx":
         docgen.write_docx(path, pw, seed)
         return [office2john.get_hash(path)]
-    if kind == "odt":
+    if kind in ("odt", "odt_e"):
+        path = os.path.join(t, "doc.odt")
         docgen.write_odt(path, pw, seed)
-        return [odt2hashes.get_hashes(path, False)]
+        return [odt2hashes.get_hashes(path, kind == "odt_e")]
     docgen.write_pdf(path, pw, seed, **kw)
     return [pdf2john.get_hash(path)]
 
@@ -70,7 +87,7 @@ def test_deep_index_round_trip(cs, n):
         assert index_of(word(i, cs, n), cs) == i
 
 
-@pytest.mark.parametrize("name,kind,kw,cs,pw,window", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("name,kind,kw,cs,pw,window", CASES + TWO_WAY, ids=[c[0] for c in CASES + TWO_WAY])
 def test_planted_documents_verify_on_the_oracle(oracle, name, kind, kw, cs, pw, window):
     with tempfile.TemporaryDirectory() as t:
         for stream in _doc_streams(t, kind, kw, pw, 0xD9F):
@@ -101,3 +118,38 @@ def test_planted_password_at_full_keyspace_positions(oracle, name, kind, kw, cs,
                 # stop_on_first returns the lowest hit of the window
                 fh, _, _ = ctx.search_range(cs, n, start, count, stop_on_first=True)
                 assert fh and min(fh) == min(hits), name
+
+
+def _window(pw, cs, window):
+    n = len(pw)
+    space = len(cs) ** n
+    idx = index_of(pw, cs)
+    start = max(0, min(idx - window // 2, space - window))
+    return idx, start, min(window, space - start)
+
+
+def test_two_way_windows_are_deep():
+    for name, kind, kw, cs, pw, window in TWO_WAY:
+        idx, start, count = _window(pw, cs, window)
+        assert start >= 2 ** 32 and count == window and start <= idx < start + count, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kind,kw,cs,pw,window", TWO_WAY, ids=[c[0] for c in TWO_WAY])
+def test_full_window_hit_set_equals_oracle(oracle, name, kind, kw, cs, pw, window):
+    """Both directions: every GPU hit is an oracle hit and every oracle hit is a GPU hit, over a complete
+    window past 2^32 at the config's charset and length; and a two-device context on the one GPU agrees."""
+    from dprf_amd import _lib
+    n = len(pw)
+    idx, start, count = _window(pw, cs, window)
+    with tempfile.TemporaryDirectory() as t:
+        for stream in _doc_streams(t, kind, kw, pw, 0xD9F):
+            want, nwant = oracle.Ctx(stream).search_range(cs, n, start, count, nthreads=ORACLE_THREADS)
+            assert idx in want, name
+            for devs in ([0], [0, 0]):
+                with _lib.Context(_fields(stream), devices=devs) as ctx:
+                    hits, nh, st = ctx.search_range(cs, n, start, count)
+                    assert st["candidates"] == count, (name, devs)
+                    assert nh == nwant and hits == want, (name, devs, len(hits), len(want))
+                    fh, _, _ = ctx.search_range(cs, n, start, count, stop_on_first=True, cap=1)
+                    assert fh == want[:1], (name, devs)

@@ -252,13 +252,14 @@ def test_brute_force_module_end_to_end(dprf, streams):
 
 
 def test_multi_device_rounds_on_one_gpu(dprf, streams, monkeypatch):
-    """The multi-device code paths (one context and one host thread per device, contiguous slices of
-    each round) run here with two contexts on the same GPU: same answers as one device, and the lowest
-    hit wins when several slices hold hits."""
+    """The multi-device code paths (one library context over a device list, one worker thread + stream per
+    entry) run here with the device list repeated on the same GPU: same answers as one device, and the
+    lowest hit wins when several devices' chunks hold hits."""
     from dprf_amd import brute_force as bf
     from dprf_amd import client as cl
     from dprf_amd import payload as pl
-    monkeypatch.setattr(bf, "ROUND_PER_DEVICE", 4096)
+    monkeypatch.setattr(bf, "FIRST_ROUND", 4096)
+    monkeypatch.setattr(bf, "ROUND_SECONDS", 0.0)
     s = streams["pdf_synth_r3_l128_abc"]["stream"]
     for devs in ([0], [0, 0], [0, 0, 0]):
         assert bf.init(s, 3, None, devices=devs) == (1, "abc")
@@ -267,8 +268,66 @@ def test_multi_device_rounds_on_one_gpu(dprf, streams, monkeypatch):
     assert bf.init(e, 4, None, devices=[0, 0, 0]) == want == (1, "bozc")
     pws = ["zzzz", "yvgl", "aaaa", "bozc", "password"]
     assert bf.init(e, 0, pws, devices=[0, 0]) == (1, "yvgl")
-    # GPU client verifier over two contexts: the lowest list index that verifies
+    # GPU client verifier over a two-device context: the lowest list index that verifies
     ver = cl.GpuVerifier([0, 0])
     blob, offs = pl._pack(pws)
     assert ver(e, blob, offs) == (1, "yvgl")
+    ver.close()
+
+
+def test_multi_device_context_equals_one_device(dprf, streams):
+    """dprf_ctx_create_devices({0,0}): two worker threads and streams on the one GPU share each call's chunk
+    cursor.  ODF -e over 2^24 alnum^5 indices (4+ launches, ~256 false hits of the 2-byte check): the
+    merged hit set equals one device's, and stop_on_first returns the lowest of them on both."""
+    from dprf_amd import brute_force as bf
+    fields = bf.parse_verification_data(streams["odt_testdoc_e"]["stream"])
+    start, count = 62 ** 5 // 3, 1 << 24
+    res = {}
+    for devs in ([0], [0, 0]):
+        with dprf.Context(fields, devices=devs) as c:
+            assert c.devices == devs
+            hits, n, st = c.search_range(ALNUM, 5, start, count, cap=1 << 12)
+            assert st["candidates"] == count and st["devices"] == len(devs) and st["launches"] >= 4
+            assert n == len(hits) and n > 16
+            fh, _, fst = c.search_range(ALNUM, 5, start, count, stop_on_first=True, cap=1)
+            assert fh == hits[:1]
+            assert fst["candidates"] >= fh[0] - start + 1     # everything below the lowest hit was verified
+            res[tuple(devs)] = hits
+    assert res[(0,)] == res[(0, 0)]
+
+
+def test_stop_on_first_lowest_across_blocks_and_launches(dprf, streams):
+    """The right password planted at several list positions spread over blocks and launches (Office: 2^19
+    candidates per launch): stop_on_first answers the lowest position, on one and on two devices, whatever
+    order the workgroups run in (a block is skipped only when its lowest index is above the lowest hit)."""
+    rng = random.Random(5)
+    n = (1 << 19) + 3000
+    words = [("".join(rng.choice(LOWER) for _ in range(6))) for _ in range(n)]
+    plant = [70001, 262143, 524290, n - 1]
+    for k in plant:
+        words[k] = "password"
+    fields_stream = streams["office_testdoc"]["stream"]
+    from dprf_amd import brute_force as bf
+    fields = bf.parse_verification_data(fields_stream)
+    for devs in ([0], [0, 0]):
+        with dprf.Context(fields, devices=devs) as c:
+            hits, nh, st = c.verify_list(words)
+            assert hits == plant and nh == len(plant) and st["launches"] >= 2
+            fh, _, fst = c.verify_list(words, stop_on_first=True, cap=1)
+            assert fh == [plant[0]] and fst["candidates"] >= plant[0] + 1
+
+
+def test_list_status_marks_only_the_invalid_candidates(dprf, streams):
+    """The GPU client drops candidates the format cannot take instead of failing the payload."""
+    from dprf_amd import client as cl
+    from dprf_amd import payload as pl
+    s = streams["office_testdoc"]["stream"]
+    pws = ["x", "", "bad\x00nul", "password", "y" * 40]
+    blob, offs = pl._pack(pws)
+    with dprf.Context(__import__("dprf_amd.brute_force", fromlist=["x"]).parse_verification_data(s)) as c:
+        st = c.list_status(blob, offs)
+        assert [int(v) for v in st] == [0, dprf.E_DOMAIN, dprf.E_INVALID, 0, dprf.E_PWLEN]
+    ver = cl.GpuVerifier([0])
+    assert ver(s, blob, offs) == (1, "password")
+    assert ver.skipped == 3
     ver.close()

@@ -102,14 +102,14 @@ class _OracleCtx:
 
     def verify_list(self, passwords, stop_on_first=False, cap=1 << 16):
         h = [i for i, p in enumerate(passwords) if self.c.verify(p.encode())]
-        return h[:cap], len(h), {}
+        return h[:cap], len(h), {"candidates": len(passwords), "wall_ms": 1.0}
 
     def search_range(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
         if self.fail_at is not None and start >= self.fail_at:
             raise KeyboardInterrupt
         self.log.append((start, count))
         h, n = self.c.search_range(charset, pwlen, start, count)
-        return h[:cap], n, {}            # absolute keyspace indices, like _lib.Context
+        return h[:cap], n, {"candidates": count, "wall_ms": 1.0}   # absolute keyspace indices, like _lib.Context
 
     def close(self):
         pass
@@ -118,17 +118,18 @@ class _OracleCtx:
 def test_range_checkpoint_resumes_where_it_stopped(streams, oracle, tmp_path, monkeypatch):
     d = streams["pdf_synth_r5_cat"]
     fields = bf.parse_verification_data(d["stream"])
-    monkeypatch.setattr(bf, "ROUND_PER_DEVICE", 1000)
+    monkeypatch.setattr(bf, "FIRST_ROUND", 1000)
+    monkeypatch.setattr(bf, "ROUND_SECONDS", 0.0)
     cp = str(tmp_path / "cursor.json")
     want = bf.LOWERCASE.index("c") * 676 + bf.LOWERCASE.index("a") * 26 + bf.LOWERCASE.index("t")
     log1 = []
-    monkeypatch.setattr(bf, "_contexts", lambda inp, dev: [_OracleCtx(oracle, d["stream"], log1, fail_at=1000)])
+    monkeypatch.setattr(bf, "_context", lambda inp, dev: _OracleCtx(oracle, d["stream"], log1, fail_at=1000))
     with pytest.raises(KeyboardInterrupt):
         bf.init_rangebased_brute_force(fields, 3, checkpoint=cp)
     assert log1 == [(0, 1000)]
     assert json.load(open(cp))["next_index"] == 1000
     log2 = []
-    monkeypatch.setattr(bf, "_contexts", lambda inp, dev: [_OracleCtx(oracle, d["stream"], log2)])
+    monkeypatch.setattr(bf, "_context", lambda inp, dev: _OracleCtx(oracle, d["stream"], log2))
     assert bf.init_rangebased_brute_force(fields, 3, checkpoint=cp) == (1, "cat")
     assert log2[0] == (1000, 1000) and log2[-1][0] <= want < log2[-1][0] + log2[-1][1]
     # finished searches answer from the checkpoint; a different search refuses it

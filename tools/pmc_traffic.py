@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Collect the dominant kernel's HBM bytes per launch from the profile summaries (tools/prof_summary.py
-output) into profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
+"""Collect the dominant kernel's PMC figures from the profile summaries (tools/prof_summary.py output):
+  profiles/pmc_traffic.json  HBM bytes per launch (FETCH_SIZE + WRITE_SIZE) -> bench.py roofline.traffic
+  profiles/pmc_valu.json     VALUBusy, VALUUtilization, LDS busy, effective clock -> bench.py roofline.valu_busy
 
 FETCH_SIZE / WRITE_SIZE come from separate rocprofv3 --pmc passes (they cannot share one on gfx950) and are
 in KiB.  MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of WIDE streaming reads (16 B/lane); none of these kernels
 streams its inputs (document constants are kernel arguments / a few KiB of tables), so no correction is
-applied.  Usage: tools/pmc_traffic.py r01 [r01b ...] (for each workload the last tag that has a profile wins)"""
+applied.  Usage: tools/pmc_traffic.py r02 [r02b ...] (for each workload the last tag that has a profile wins)"""
 import json
 import os
 import sys
@@ -13,8 +14,8 @@ import sys
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOM = {"odt": "k_odt_kdf", "odt_e": "k_odt_kdf", "office": "k_office_kdf", "pdf_r34": "k_pdf_r24",
        "pdf_r2": "k_pdf_r24", "pdf_r5": "k_pdf_r5", "pdf_r6": "k_pdf_r6"}
-tags = sys.argv[1:] or ["r01"]
-out = {}
+tags = sys.argv[1:] or ["r02"]
+traffic, valu = {}, {}
 for w, kname in DOM.items():
     f = None
     for tag in tags:
@@ -25,10 +26,19 @@ for w, kname in DOM.items():
         continue
     d = json.load(open(f))
     for k, v in d.get("counters", {}).items():
-        if kname in k:
-            pd = v["per_dispatch"]
-            out[w] = {"kernel": k, "bytes_per_launch": v.get("hbm_bytes_per_dispatch"),
-                      "fetch_bytes": pd.get("FETCH_SIZE", 0) * 1024, "write_bytes": pd.get("WRITE_SIZE", 0) * 1024,
-                      "source": os.path.relpath(f, HERE)}
-json.dump(out, open(os.path.join(HERE, "profiles", "pmc_traffic.json"), "w"), indent=1)
-print(json.dumps(out, indent=1))
+        if kname not in k:
+            continue
+        pd = v["per_dispatch"]
+        src = os.path.relpath(f, HERE)
+        if v.get("hbm_bytes_per_dispatch") is not None:
+            traffic[w] = {"kernel": k, "bytes_per_launch": v.get("hbm_bytes_per_dispatch"),
+                          "fetch_bytes": pd.get("FETCH_SIZE", 0) * 1024, "write_bytes": pd.get("WRITE_SIZE", 0) * 1024,
+                          "source": src}
+        if v.get("valu_busy") is not None:
+            valu[w] = {"kernel": k, "valu_busy": v.get("valu_busy"), "valu_utilization": v.get("valu_utilization"),
+                       "lds_busy": v.get("lds_busy"), "effective_clock_GHz": v.get("effective_clock_GHz"),
+                       "valu_active_per_wave_cycle": v.get("valu_active_per_wave_cycle"),
+                       "SQ_LDS_BANK_CONFLICT_per_launch": pd.get("SQ_LDS_BANK_CONFLICT"), "source": src}
+for name, obj in (("pmc_traffic.json", traffic), ("pmc_valu.json", valu)):
+    json.dump(obj, open(os.path.join(HERE, "profiles", name), "w"), indent=1)
+print(json.dumps({"traffic": traffic, "valu": valu}, indent=1))

@@ -1,6 +1,16 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile_gpu.sh run into profiles/<name>.json + the kernel_stats csv.
-Usage: tools/prof_summary.py gpurun_out/prof_odt_r01 profiles/prof_odt_r01"""
+Usage: tools/prof_summary.py gpurun_out/prof_odt_r02 profiles/prof_odt_r02
+
+Counters are kept per --pmc pass (each pass is its own run of the program), averaged over the dispatches of
+each kernel, and the derived metrics are computed within one pass:
+  valu_busy        = SQ_ACTIVE_INST_VALU * 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs)   (ROCm's VALUBusy formula,
+                     derived_counters.xml; GRBM_GUI_ACTIVE is summed over the 8 XCDs on gfx950,
+                     MI355X_MICROARCH.md)
+  valu_utilization = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)           (ROCm's VALUUtilization)
+  lds_busy         = SQ_ACTIVE_INST_LDS * 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs)    (same form, LDS instructions)
+  effective_clock  = GRBM_GUI_ACTIVE / XCDs / kernel duration
+"""
 import collections
 import csv
 import json
@@ -8,47 +18,67 @@ import os
 import shutil
 import sys
 
-src, dst = sys.argv[1], sys.argv[2]
-os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
-out = {"source": src}
-kt = os.path.join(src, "kt", "kt_kernel_stats.csv")
-if os.path.exists(kt):
-    shutil.copy(kt, dst + "_kernel_stats.csv")
-    out["kernel_stats"] = [dict(r) for r in csv.DictReader(open(kt))]
-bench = os.path.join(src, "bench_under_kt.json")
-if os.path.exists(bench):
-    out["bench_under_profiler"] = json.load(open(bench))
-counters = collections.defaultdict(lambda: collections.defaultdict(float))
-dispatches = collections.defaultdict(set)
-durations = collections.defaultdict(dict)
-for sub in ("fetch", "write", "sq", "lds"):
-    f = os.path.join(src, sub, sub + "_counter_collection.csv")
-    if not os.path.exists(f):
-        continue
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
-        if k.startswith("__amd"):
+SIMDS, XCDS = 256 * 4, 8
+PASSES = ("fetch", "write", "sq", "lds")
+
+
+def summarize(src, dst):
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+    out = {"source": src}
+    kt = os.path.join(src, "kt", "kt_kernel_stats.csv")
+    if os.path.exists(kt):
+        shutil.copy(kt, dst + "_kernel_stats.csv")
+        out["kernel_stats"] = [dict(r) for r in csv.DictReader(open(kt))]
+    bench = os.path.join(src, "bench_under_kt.json")
+    if os.path.exists(bench):
+        try:
+            out["bench_under_profiler"] = json.load(open(bench))
+        except ValueError:
+            pass
+    # kernel -> pass -> counter -> {dispatch: value}
+    raw = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(dict)))
+    dur = collections.defaultdict(lambda: collections.defaultdict(dict))
+    for sub in PASSES:
+        f = os.path.join(src, sub, sub + "_counter_collection.csv")
+        if not os.path.exists(f):
             continue
-        counters[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        dispatches[k + "/" + sub].add(r["Dispatch_Id"])
-        durations[k][(sub, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-summ = {}
-for k, c in counters.items():
-    n = max(len(dispatches.get(k + "/" + s, ())) for s in ("fetch", "write", "sq", "lds"))
-    d = {name: v / max(1, len(dispatches.get(k + "/" + sub, ()) or [1]))
-         for name, v in c.items()
-         for sub in [("fetch" if name == "FETCH_SIZE" else "write" if name == "WRITE_SIZE" else
-                      "sq" if name in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
-                                       "SQ_WAVES", "GRBM_GUI_ACTIVE") else "lds")]}
-    per = {"per_dispatch": d, "dispatches_per_pass": n}
-    sq_durs = [v for (sub, _), v in durations[k].items() if sub == "sq"]
-    if "GRBM_GUI_ACTIVE" in d and sq_durs:
-        per["effective_clock_GHz"] = d["GRBM_GUI_ACTIVE"] / 8 / (sum(sq_durs) / len(sq_durs))
-    if "FETCH_SIZE" in d or "WRITE_SIZE" in d:
-        # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads 1/2 of wide streaming reads
-        # (MI355X_MICROARCH.md HBM section) -- these kernels have no streaming reads, so no correction.
-        per["hbm_bytes_per_dispatch"] = (d.get("FETCH_SIZE", 0) + d.get("WRITE_SIZE", 0)) * 1024
-    summ[k] = per
-out["counters"] = summ
-json.dump(out, open(dst + ".json", "w"), indent=1)
-print(json.dumps(summ, indent=1))
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0]
+            if k.startswith("__amd"):
+                continue
+            d = r["Dispatch_Id"]
+            raw[k][sub][r["Counter_Name"]][d] = raw[k][sub][r["Counter_Name"]].get(d, 0.0) + float(r["Counter_Value"])
+            dur[k][sub][d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    summ = {}
+    for k, passes in raw.items():
+        per = {"per_dispatch": {}, "passes": {}}
+        for sub, ctrs in passes.items():
+            avg = {name: sum(v.values()) / len(v) for name, v in ctrs.items()}
+            ns = sum(dur[k][sub].values()) / max(1, len(dur[k][sub]))
+            per["passes"][sub] = dict(avg, kernel_ns=ns, dispatches=len(dur[k][sub]))
+            per["per_dispatch"].update(avg)
+            g = avg.get("GRBM_GUI_ACTIVE")
+            if g:
+                cyc = g / XCDS
+                per.setdefault("effective_clock_GHz", cyc / ns if ns else None)
+                if "SQ_ACTIVE_INST_VALU" in avg:
+                    per["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / cyc
+                if "SQ_ACTIVE_INST_LDS" in avg:
+                    per["lds_busy"] = avg["SQ_ACTIVE_INST_LDS"] * 4 / SIMDS / cyc
+            if avg.get("SQ_THREAD_CYCLES_VALU") and avg.get("SQ_ACTIVE_INST_VALU"):
+                per["valu_utilization"] = avg["SQ_THREAD_CYCLES_VALU"] / (avg["SQ_ACTIVE_INST_VALU"] * 64)
+            if avg.get("SQ_ACTIVE_INST_VALU") and avg.get("SQ_WAVE_CYCLES"):
+                per["valu_active_per_wave_cycle"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+        pd = per["per_dispatch"]
+        if "FETCH_SIZE" in pd or "WRITE_SIZE" in pd:
+            # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads 1/2 of wide streaming
+            # reads (MI355X_MICROARCH.md HBM section) -- these kernels have no streaming reads, no correction.
+            per["hbm_bytes_per_dispatch"] = (pd.get("FETCH_SIZE", 0) + pd.get("WRITE_SIZE", 0)) * 1024
+        summ[k] = per
+    out["counters"] = summ
+    json.dump(out, open(dst + ".json", "w"), indent=1)
+    return summ
+
+
+if __name__ == "__main__":
+    print(json.dumps(summarize(sys.argv[1], sys.argv[2]), indent=1))

@@ -5,14 +5,15 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 W=${1:-odt}
-TAG=${2:-r01}
+TAG=${2:-r02}
 OUT=$R/gpurun_out/prof_${W}_${TAG}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 BENCH="$R/bench.py --workload $W --no-side --cpu-seconds 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $BENCH --steps 3 --warmup 1 > $OUT/bench_under_kt.json
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o fetch --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o write --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d $OUT/sq -o sq --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_ANY --kernel-trace -d $OUT/lds -o lds --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o fetch --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o write --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
+timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d $OUT/sq -o sq --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
+timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d $OUT/lds -o lds --output-format csv -- python3 $BENCH --steps 1 --warmup 0 > /dev/null
+python3 $R/tools/prof_summary.py $OUT $R/gpurun_out/summary_${W}_${TAG} > /dev/null
 find $OUT -name "*.csv"
