@@ -218,7 +218,7 @@ def shard(step, rank, world, batch, space):
     return start, min(batch, space - start)
 
 
-def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, batch=None, ndev=1):
+def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, batch=None, ndev=1, stop_on_first=False):
     """W untimed + K timed steps of `name` on this rank.  A step verifies B consecutive indices per GPU
     (ndev GPUs in this process: one multi-device library call covers ndev * B) through
     brute_force.search_round -- the exact call the product's range mode makes per round -- then the ranks
@@ -235,7 +235,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
 
     def step(s):
         start, n = shard(s, rank, world, B, space)
-        idx, st = brute_force.search_round(ctx, cs, pwlen, start, n)
+        idx, st = brute_force.search_round(ctx, cs, pwlen, start, n, stop_on_first=stop_on_first)
         return allreduce_min(idx if idx is not None else (1 << 62)), st
 
     for s in range(warmup):
@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU candidates per step (default per workload)")
     ap.add_argument("--no-side", action="store_true", help="skip the per-format side measurements")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--stop-on-first", action="store_true",
+                    help="time the product's early-stop rounds instead of full verification of every batch")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -352,7 +354,7 @@ def main():
     ctx = _lib.Context(fields, devices=devices)
     B = args.batch or B
     dt, stats, lowest, pwlen = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync,
-                                            allreduce_min, B, ndev=len(devices))
+                                            allreduce_min, B, ndev=len(devices), stop_on_first=args.stop_on_first)
     dt_max = allreduce_max(dt)
     m = summarize(stats, wkey, world, dt_max)
     peak = work.PEAK_LANE_INSTR_PER_S

@@ -125,10 +125,11 @@ def next_round(rate, remaining, seconds=ROUND_SECONDS):
     return min(remaining, n)
 
 
-def search_round(ctx, charset, pwlen, start, count):
+def search_round(ctx, charset, pwlen, start, count, stop_on_first=True):
     """One round of range mode on every device of ctx: (lowest hit index or None, stats).  The same call
-    bench.py times per rank."""
-    hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=True, cap=1)
+    bench.py times per rank (there with stop_on_first=False: a throughput step verifies its whole batch
+    even when a false positive of ODF -e's 2-byte check turns up in it)."""
+    hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
     return (hits[0] if hits else None), st
 
 

@@ -322,11 +322,14 @@ static int parse_pdf(dprf_ctx *c, const char *const *f) {
  * full generation of k_office_kdf (256 CUs x 32 waves x 64 lanes); R6's persistent workgroups need ~8
  * candidates per slot per launch to amortise the round-length tail. */
 struct chunk_policy { uint32_t init, lo, hi; double target_ms; };
+#ifndef DPRF_R24_HI_LOG2
+#define DPRF_R24_HI_LOG2 30
+#endif
 static chunk_policy policy(kernel_kind k) {
     switch (k) {
         case K_OFFICE: return {1u << 19, 1u << 19, 1u << 20, 400.0};
         case K_ODT: return {1u << 22, 1u << 19, 1u << 23, 300.0};
-        case K_PDF_R24: return {1u << 24, 1u << 20, 1u << 30, 100.0};
+        case K_PDF_R24: return {1u << 24, 1u << 20, 1u << DPRF_R24_HI_LOG2, 100.0};
         case K_PDF_R5: return {1u << 27, 1u << 22, 1u << 31, 100.0};
         case K_PDF_R6: return {1u << 21, 1u << 20, 1u << 22, 1000.0};
         default: return {1u << 24, 1u << 20, 1u << 24, 100.0};
@@ -510,7 +513,7 @@ static void atomic_min_u64(std::atomic<uint64_t> &a, uint64_t v) {
 struct lane_result {
     std::vector<unsigned long long> hits;
     uint32_t nhits = 0;
-    uint64_t first = ~0ull, evaluated = 0, launches = 0;
+    uint64_t first = ~0ull, evaluated = 0, launches = 0, launched = 0;
     double kms = 0, mms = 0;
 };
 
@@ -577,6 +580,7 @@ static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_resu
             (e = hipMemcpyAsync(&L.h_ring[s], L.d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, L.stream)) != hipSuccess ||
             (e = hipEventRecord(L.ev[s][3], L.stream)) != hipSuccess) { failed = "launch bookkeeping"; break; }
         nchunk[s] = n;
+        out.launched += n;
         inq++;
     }
     while (inq > 0) {
@@ -588,7 +592,7 @@ static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_resu
         (e = hipStreamSynchronize(L.stream)) != hipSuccess) { hip_fail("result header", e); return; }
     out.nhits = fin->nhits;
     out.first = fin->first;
-    out.evaluated = fin->evaluated;
+    out.evaluated = out.launched - fin->skipped;
     const uint32_t ncopy = std::min<uint32_t>(out.nhits, DEV_HIT_CAP);
     out.hits.resize(ncopy);
     if (ncopy &&

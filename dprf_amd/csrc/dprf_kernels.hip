@@ -72,8 +72,10 @@ DEVI void get_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand 
  * With stop_on_first a block is skipped only when its LOWEST candidate index lies above the lowest hit
  * found so far (R->first): every index below the final `first` is then verified whatever order the
  * workgroups are dispatched in, so the reported hit is the lowest of the call unconditionally (a boolean
- * stop flag would let a late-dispatched lower block skip itself).  `per` = candidates per thread. */
-template <bool AES>
+ * stop flag would let a late-dispatched lower block skip itself).  `per` = candidates per thread.
+ * COUNT: this kernel's skipped blocks are counted in R->skipped (the verifying kernel of a format; the
+ * KDF kernels of Office/ODF skip exactly the blocks their check kernel skips and do not count). */
+template <bool AES, bool COUNT = true>
 DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_results *R, uint32_t stop_on_first,
                          uint8_t *cs, aes_lds *L, uint32_t *flag, uint32_t per = 1) {
     const uint32_t tid = threadIdx.x;
@@ -88,8 +90,12 @@ DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_resu
     if (tid == 0) {
         uint32_t skip = 0u;
         if (stop_on_first) {
-            const unsigned long long base = e.start + (unsigned long long)blockIdx.x * blockDim.x * per;
-            skip = base > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+            const uint32_t off = blockIdx.x * blockDim.x * per;
+            skip = e.start + off > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+            if (skip && COUNT) {
+                const uint32_t n = e.count - off < blockDim.x * per ? e.count - off : blockDim.x * per;
+                atomicAdd(&R->skipped, (unsigned long long)n);
+            }
         }
         *flag = skip;
     }
@@ -102,14 +108,6 @@ DEVI void report_hit(dprf_results *R, unsigned long long idx, uint32_t cap, uint
     if (slot < cap) R->hits[slot] = idx;
     atomicMin(&R->first, idx);
     if (stop_on_first) atomicExch(&R->stop, 1u);
-}
-
-DEVI void count_block(const dprf_enum &e, dprf_results *R) {
-    if (threadIdx.x == 0) {
-        uint32_t base = blockIdx.x * blockDim.x;
-        uint32_t n = e.count - base < blockDim.x ? e.count - base : blockDim.x;
-        atomicAdd(&R->evaluated, (unsigned long long)n);
-    }
 }
 
 /* BE message words of `len` candidate bytes (LE-packed) placed after `pre` bytes already in m[],
@@ -160,7 +158,7 @@ __global__ void __launch_bounds__(256, 8)
 k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
-    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
+    if (!block_prologue<false, false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (g0 >= e.count) return;
     const uint32_t g = g0;
@@ -239,7 +237,6 @@ k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf
     }
     ok = ok && vh[0] == dh0[0] && vh[1] == dh0[1] && vh[2] == dh0[2] && vh[3] == dh0[3] && vh[4] == dh1[0];
     if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
-    count_block(e, R);
 }
 
 /* ================================================================== ODF 1.2 (AES-256-CBC, PBKDF2-HMAC-SHA1) */
@@ -250,7 +247,7 @@ __global__ void __launch_bounds__(256, 8)
 k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
-    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
+    if (!block_prologue<false, false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag)) return;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (g0 >= e.count) return;
     const uint32_t g = g0;
@@ -417,7 +414,6 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
         for (int k = 0; k < 8; k++) ok = ok && st[k] == p.checksum[k];
     }
     if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
-    count_block(e, R);
 }
 
 /* ================================================================== PDF R5 (one SHA-256) */
@@ -520,10 +516,6 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) ok = ok && hh[kk] == p.u[kk];
         if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t n = e.count - base < blockDim.x * R5_PER ? e.count - base : blockDim.x * R5_PER;
-        atomicAdd(&R->evaluated, (unsigned long long)n);
     }
 }
 
@@ -889,10 +881,6 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             }
         }
         if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t n = e.count - base < 64u * PER ? e.count - base : 64u * PER;
-        atomicAdd(&R_->evaluated, (unsigned long long)n);
     }
 }
 

@@ -337,7 +337,6 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 
 struct r6_shared {
     uint32_t hist[8];
-    uint32_t done;                      /* candidates finished by this workgroup */
     uint32_t nslots, te_slots, pad;
     uint16_t bstart[R6_MAX_BATCHES];    /* batch b = order[bstart[b] .. bstart[b] + bsize[b]) */
     uint8_t bsize[R6_MAX_BATCHES];
@@ -370,9 +369,12 @@ DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
      * been taken and will finish: skipping those above the lowest hit so far (stop_on_first) keeps the
      * reported hit the lowest of the call */
     uint32_t c = atomicAdd(&R->cursor, 1u);
-    if (c >= e.count ||
-        (stop_on_first && e.start + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+    if (c >= e.count) {
         c = R6_IDLE;
+    } else if (stop_on_first && e.start + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        atomicAdd(&R->skipped, 1ull);
+        c = R6_IDLE;
+    }
     sh->cand[slot] = c;
     if (c != R6_IDLE) {
         uint32_t K[16];
@@ -410,7 +412,6 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = T->te0[k >> 5];
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     if (tid < 8) sh->hist[tid] = 0u;
-    if (tid == 0) sh->done = 0u;
     __syncthreads();
 
     for (uint32_t sl = tid; sl < nslots; sl += nthr)
@@ -519,7 +520,6 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     atomicMin(&R->first, idx);
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
-                atomicAdd(&sh->done, 1u);
                 r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);
@@ -531,7 +531,6 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         printf("r6 timing wg %u wave %u: work %llu fam %llu barrier %llu | sha256 batches %llu units %llu cyc %llu | sha512 batches %llu units %llu cyc %llu\n",
                blockIdx.x, tid >> 6, t_work, t_fam, t_bar, t_nb[0], t_units[0], t_cyc[0], t_nb[1], t_units[1], t_cyc[1]);
 #endif
-    if (tid == 0 && sh->done) atomicAdd(&R->evaluated, (unsigned long long)sh->done);
 }
 
 /* Slot capacity of one workgroup: 32-slot groups in the upper halves of the Te0 rows, then 64-slot groups

@@ -33,7 +33,10 @@ struct dprf_results {
     uint32_t cursor;                /* work cursor of persistent kernels (PDF R6), reset per launch */
     uint32_t pad_;
     unsigned long long first;       /* lowest hit index (atomicMin), ~0 if none */
-    unsigned long long evaluated;   /* candidates evaluated (per-block atomicAdd) */
+    unsigned long long skipped;     /* candidates of launched chunks NOT evaluated: stop_on_first blocks
+                                       skipped above the lowest hit (rare: one atomic per skipped block, none
+                                       per evaluated block -- a per-block counter on this line made every
+                                       block's `first` load wait behind the atomics, -25 % on PDF R2) */
     unsigned long long hits[1];     /* [cap] */
 };
 
