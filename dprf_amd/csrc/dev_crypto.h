@@ -145,33 +145,44 @@ DEVI constexpr uint64_t k512(int t) {
     0x4cc5d4becb3e42b6ull,0x597f299cfc657e2aull,0x5fcb6fab3ad6faecull,0x6c44198c4a475817ull};
     return K[t];
 }
-/* 64-bit rotate / shift on the two 32-bit halves with v_alignbit_b32 (2 slots each): the compiler's own
- * lowering (v_lshrrev_b64 + v_lshl_add_u64) costs ~4.6 + 2.6 slots, measured (profiles/valu_issue_rates). */
-DEVI uint64_t pack64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+/* 64-bit values are VGPR pairs built from two 32-bit halves with a bit-cast (no arithmetic: the pair is
+ * just a REG_SEQUENCE).  Rotates / shifts work on the halves with v_alignbit_b32 (2 slots each; the
+ * compiler's own v_lshrrev_b64 costs 4.6), and every 64-bit addition is ONE v_lshl_add_u64 in inline asm
+ * (2.6 slots, tools/valu_peak.hip): written as plain `+` on a value assembled as (hi << 32) | lo, LLVM
+ * split each add into two v_lshl_add_u64 of the zero-extended halves plus two v_mov -- 1,202 instead of
+ * ~760 adds and 453 moves per SHA-512 compression (8,444 -> ~6,800 slots). */
+DEVI uint64_t pack64(uint32_t hi, uint32_t lo) { return __builtin_bit_cast(uint64_t, make_uint2(lo, hi)); }
+DEVI uint32_t lo32(uint64_t x) { return __builtin_bit_cast(uint2, x).x; }
+DEVI uint32_t hi32(uint64_t x) { return __builtin_bit_cast(uint2, x).y; }
+DEVI uint64_t add64(uint64_t a, uint64_t b) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+/* a + k for a compile-time constant k: the constant goes in an SGPR pair (SALU s_mov, no VALU slot) */
+DEVI uint64_t add64k(uint64_t a, uint64_t k) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "s"(k));
+    return r;
+}
 DEVI uint64_t ror64(uint64_t x, int s) {
-    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t lo = lo32(x), hi = hi32(x);
     if (s == 32) return pack64(lo, hi);
     if (s < 32) return pack64(__builtin_amdgcn_alignbit(lo, hi, s), __builtin_amdgcn_alignbit(hi, lo, s));
     return pack64(__builtin_amdgcn_alignbit(hi, lo, s - 32), __builtin_amdgcn_alignbit(lo, hi, s - 32));
 }
 DEVI uint64_t shr64(uint64_t x, int s) {   /* 0 < s < 32 */
-    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t lo = lo32(x), hi = hi32(x);
     return pack64(hi >> s, __builtin_amdgcn_alignbit(hi, lo, s));
 }
 DEVI uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
-    uint32_t lo = xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
-    uint32_t hi = xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    return pack64(xor3(hi32(a), hi32(b), hi32(c)), xor3(lo32(a), lo32(b), lo32(c)));
 }
 DEVI uint64_t ch64(uint64_t a, uint64_t b, uint64_t c) {
-    uint32_t lo = f_ch((uint32_t)a, (uint32_t)b, (uint32_t)c);
-    uint32_t hi = f_ch((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    return pack64(f_ch(hi32(a), hi32(b), hi32(c)), f_ch(lo32(a), lo32(b), lo32(c)));
 }
 DEVI uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
-    uint32_t lo = f_maj((uint32_t)a, (uint32_t)b, (uint32_t)c);
-    uint32_t hi = f_maj((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    return pack64(f_maj(hi32(a), hi32(b), hi32(c)), f_maj(lo32(a), lo32(b), lo32(c)));
 }
 DEVI void sha512_iv(uint64_t st[8], bool is384) {
     if (is384) {
@@ -192,19 +203,20 @@ DEVI void sha512_compress(uint64_t st[8], uint64_t w[16]) {
         if (t < 16) {
             wt = w[t];
         } else {
-            uint64_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
-            uint64_t s0 = xor3_64(ror64(x, 1), ror64(x, 8), shr64(x, 7));
-            uint64_t s1 = xor3_64(ror64(y, 19), ror64(y, 61), shr64(y, 6));
-            wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+            const uint64_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
+            const uint64_t s0 = xor3_64(ror64(x, 1), ror64(x, 8), shr64(x, 7));
+            const uint64_t s1 = xor3_64(ror64(y, 19), ror64(y, 61), shr64(y, 6));
+            wt = add64(add64(w[t & 15], s0), add64(w[(t - 7) & 15], s1));
             w[t & 15] = wt;
         }
-        uint64_t S1 = xor3_64(ror64(e, 14), ror64(e, 18), ror64(e, 41));
-        uint64_t t1 = h + S1 + ch64(e, f, g) + (k512(t) + wt);
-        uint64_t S0 = xor3_64(ror64(a, 28), ror64(a, 34), ror64(a, 39));
-        uint64_t t2 = S0 + maj64(a, b, c);
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        const uint64_t S1 = xor3_64(ror64(e, 14), ror64(e, 18), ror64(e, 41));
+        const uint64_t t1 = add64(add64(h, S1), add64(ch64(e, f, g), add64k(wt, k512(t))));
+        const uint64_t S0 = xor3_64(ror64(a, 28), ror64(a, 34), ror64(a, 39));
+        const uint64_t t2 = add64(S0, maj64(a, b, c));
+        h = g; g = f; f = e; e = add64(d, t1); d = c; c = b; b = a; a = add64(t1, t2);
     }
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    st[0] = add64(st[0], a); st[1] = add64(st[1], b); st[2] = add64(st[2], c); st[3] = add64(st[3], d);
+    st[4] = add64(st[4], e); st[5] = add64(st[5], f); st[6] = add64(st[6], g); st[7] = add64(st[7], h);
 }
 
 /* ------------------------------------------------------------------ MD5 (RFC 1321 3.4) */

@@ -115,14 +115,14 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
 DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const uint32_t hi[16]) {
     uint64_t st[8], w[16];
 #pragma unroll
-    for (int k = 0; k < 8; k++) st[k] = ((uint64_t)hs[2 * k] << 32) | hs[2 * k + 1];
+    for (int k = 0; k < 8; k++) st[k] = pack64(hs[2 * k], hs[2 * k + 1]);
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = ((uint64_t)lo[2 * k] << 32) | lo[2 * k + 1];
+    for (int k = 0; k < 8; k++) w[k] = pack64(lo[2 * k], lo[2 * k + 1]);
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[8 + k] = ((uint64_t)hi[2 * k] << 32) | hi[2 * k + 1];
+    for (int k = 0; k < 8; k++) w[8 + k] = pack64(hi[2 * k], hi[2 * k + 1]);
     sha512_compress(st, w);
 #pragma unroll
-    for (int k = 0; k < 8; k++) { hs[2 * k] = (uint32_t)(st[k] >> 32); hs[2 * k + 1] = (uint32_t)st[k]; }
+    for (int k = 0; k < 8; k++) { hs[2 * k] = hi32(st[k]); hs[2 * k + 1] = lo32(st[k]); }
 }
 
 /* Load candidate `idx` (keyspace index or slot), compute K = SHA256(pw || salt), write pw to the
