@@ -590,6 +590,12 @@ static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_resu
     if (failed) { hip_fail(failed, e); return; }
     if ((e = hipMemcpyAsync(fin, L.d_res, sizeof(dprf_results), hipMemcpyDeviceToHost, L.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(L.stream)) != hipSuccess) { hip_fail("result header", e); return; }
+    if (fin->pad_) {
+        snprintf(buf, sizeof buf, "%s kernel flagged an internal error (0x%x) on device %d", kind_name(c->kind),
+                 fin->pad_, L.device);
+        cs.error(DPRF_E_HIP, buf);
+        return;
+    }
     out.nhits = fin->nhits;
     out.first = fin->first;
     out.evaluated = out.launched - fin->skipped;

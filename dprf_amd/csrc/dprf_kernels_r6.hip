@@ -304,22 +304,27 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
     return prev[3] & 0xffu;
 }
 
-/* Slots, classes and batches.  One workgroup per CU (12 waves) holds up to R6_MAX_SLOTS candidates
- * ("slots") -- more slots than lanes; everything a slot needs between rounds is in LDS: its period
- * (pw || K[0:bs] || wrap) in a column of a pattern area, a state word and its candidate number.  Each
- * interval:
- *  1. every live slot finds the hash family of its next round (one AES block) and is counting-sorted by
- *     class = (family is SHA-256 ? 0 : 3) + (bs - 32) / 16 (the data length is 64 x (len + bs));
- *  2. each family's sorted slots are cut into batches of 64 consecutive slots (one family per batch, the
- *     trip count of a batch is that of its longest period), costed per 64-byte unit of their family and
- *     listed costliest first;
- *  3. each wave repeatedly takes the next batch of that list (an LDS counter) and runs one round of it
- *     (greedy list scheduling: a wave that runs faster because fewer waves share its SIMD takes more),
- *     then all meet at the barrier.
- * With slots = lanes and one batch per wave (the previous schedule), waves of cheap classes sat 37 % of
- * the time at the barrier (profiles/r6_round_timing_r01.txt); with ~1.6x as many slots as lanes the
- * list scheduling evens the waves' loads.  A finished slot takes the next candidate of the launch from a global
- * cursor, so no workgroup idles while another still has work.
+/* Slots and classes.  One workgroup per CU (12 waves) holds up to R6_MAX_SLOTS candidates ("slots") --
+ * more slots than lanes; everything a slot needs between rounds is in LDS: its period (pw || K[0:bs] ||
+ * wrap) in a column of a pattern area, a state word and its candidate number.  A round costs
+ * 64 x (len + bs) bytes of AES-CBC + a SHA-256 or SHA-384/512 pass over them, and the family is only known
+ * after the round's first ciphertext block, so a wave runs a round for 64 slots of ONE class
+ * (class = (family is SHA-256 ? 0 : 3) + (bs - 32) / 16: same hash code, same trip count).
+ *
+ * Flow scheduling, no barriers: a slot that finishes its round (or starts a candidate) computes the family
+ * of its next round (one AES block) and is queued in its class's bitmap; a wave that is free claims up to
+ * 64 queued slots of the fullest class (bitmap words, atomicAnd) and runs one round of them.  Waves
+ * never wait for each other.  The previous schedule -- all slots sorted per interval, batches listed
+ * costliest first, a workgroup barrier per interval -- left 16 % of wave time at the barriers
+ * (-DDPRF_R6_TIMING): ~20 batches of 1-2 M cycles over 12 waves leave a long tail every interval.
+ *
+ * Deadlock freedom (the round-1 lock-based queue hung): there is no lock and no wave ever waits on a value
+ * only another waiting wave could produce.  Every claim is one wave-uniform pass (lane 0's decisions
+ * broadcast by readfirstlane), so no lane of a wave spins while another lane of the same wave holds
+ * something; a wave that finds nothing queued sleeps and re-reads (atomic loads, never hoisted) only while
+ * `live` > 0, i.e. while some other wave is running a round whose slots it will queue or retire.  `live`
+ * (slots holding a candidate) only falls when a slot finds the launch's cursor exhausted; at 0 every wave
+ * leaves the loop, and the grid drains.
  *
  * Pattern areas: slots [0, te_slots) live in the free upper halves of the Te0 rows in groups of 32
  * (column 128 + 4*(slot%32)), the rest in the dynamic area in groups of 64 (column 4*(slot%64)); rows are
@@ -327,25 +332,22 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #ifndef R6_LANES
 #define R6_LANES 768
 #endif
-#define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
 #ifndef R6_MAX_SLOTS
 #define R6_MAX_SLOTS 1280
 #endif
-#define R6_CLASSES 7                    /* 6 live classes + "no candidate" */
+#define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
+#define R6_CLASSES 6
+#define R6_MAP_WORDS ((R6_MAX_SLOTS + 31) / 32)
 #define R6_IDLE 0xffffffffu
-#define R6_MAX_BATCHES (R6_MAX_SLOTS / 64 + 2)
 
 struct r6_shared {
-    uint32_t hist[8];
+    uint32_t map[R6_CLASSES][R6_MAP_WORDS];   /* queued slots of each class, one bit per slot          */
+    uint32_t count[R6_CLASSES];               /* queued slots per class (a hint for picking the class) */
+    uint32_t live;                            /* slots holding a candidate                             */
     uint32_t nslots, te_slots, pad;
-    uint16_t bstart[R6_MAX_BATCHES];    /* batch b = order[bstart[b] .. bstart[b] + bsize[b]) */
-    uint8_t bsize[R6_MAX_BATCHES];
-    uint32_t bcost[R6_MAX_BATCHES];
-    uint32_t nbatches, next_batch;      /* batches of this interval; the next one a wave takes */
-    uint8_t ids[R6_MAX_BATCHES];        /* batch ids, costliest first */
-    uint32_t state[R6_MAX_SLOTS];       /* len | bs << 8 | round << 16 | family << 30 */
-    uint32_t cand[R6_MAX_SLOTS];        /* candidate offset within the launch, R6_IDLE when none */
-    uint16_t order[R6_MAX_SLOTS];       /* slots sorted by class */
+    uint16_t stage[R6_LANES / 64][64];        /* per wave: the slot ids of the batch it claimed         */
+    uint32_t state[R6_MAX_SLOTS];             /* len | bs << 8 | round << 16                            */
+    uint32_t cand[R6_MAX_SLOTS];              /* candidate offset within the launch, R6_IDLE when none  */
 };
 
 DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, uint32_t slot, uint32_t lane) {
@@ -363,7 +365,7 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
 }
 
 template <int MODE>
-DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, dprf_results *R,
+DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, dprf_results *R,
                    uint32_t stop_on_first, r6_shared *sh, const r6_lds &S, uint32_t slot) {
     /* the cursor hands out candidates in increasing order, so every candidate below one that is taken has
      * been taken and will finish: skipping those above the lowest hit so far (stop_on_first) keeps the
@@ -376,22 +378,79 @@ DEVI void r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
         c = R6_IDLE;
     }
     sh->cand[slot] = c;
-    if (c != R6_IDLE) {
-        uint32_t K[16];
-        const uint32_t len = r6_begin<MODE>(e, p, cs, e.start + c, S, K);
-        r6_store_k(S, len, 32u, K);
-        sh->state[slot] = len | (32u << 8);
-    }
+    if (c == R6_IDLE) return false;
+    uint32_t K[16];
+    const uint32_t len = r6_begin<MODE>(e, p, cs, e.start + c, S, K);
+    r6_store_k(S, len, 32u, K);
+    sh->state[slot] = len | (32u << 8);
+    return true;
 }
 
-/* cost of one round of a batch whose longest period is Lp, in units of ~1/64 issue slot:
- * per 64-byte unit 4 AES blocks + 1 SHA-256c (4 x 478 + 2446) or half a SHA-512c (4 x 478 + 3186) */
-DEVI uint32_t r6_cost(uint32_t family_group, uint32_t Lp) { return Lp * (family_group ? 5098u : 4358u); }
+/* Queue a slot holding a candidate in the class of its next round. */
+DEVI void r6_push(r6_shared *sh, const r6_lds &S, uint32_t slot) {
+    const uint32_t st = sh->state[slot];
+    const uint32_t fam = r6_family(S, st & 0xffu);
+    const uint32_t cls = (fam ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
+    sh->state[slot] = (st & 0x3fffffffu) | (fam << 30);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");         /* state/period before the bit */
+    atomicOr(&sh->map[cls][slot >> 5], 1u << (slot & 31u));
+    atomicAdd(&sh->count[cls], 1u);
+}
+
+DEVI uint32_t lds_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+/* Wave-uniform: claim up to 64 queued slots of the fullest class; returns how many (0: none queued) and
+ * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
+ * order up to 64 in total, clear exactly the bits they chose (atomicAnd returns what they got when another
+ * wave raced them), and the ids are handed out through the wave's stage row. */
+DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot) {
+    const uint32_t cnt = lane < R6_CLASSES ? lds_load(&sh->count[lane]) : 0u;
+    uint32_t best = R6_CLASSES, bc = 0;
+#pragma unroll
+    for (int c = 0; c < R6_CLASSES; c++) {
+        const uint32_t v = __builtin_amdgcn_readlane(cnt, c);
+        if (v > bc) { bc = v; best = c; }
+    }
+    if (bc == 0) return 0;
+    const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
+    const uint32_t pc = __builtin_popcount(w);
+    /* inclusive scan of the word popcounts over the wave */
+    uint32_t inc = pc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += o;
+    }
+    /* whole words while the running total stays <= 64; the word that crosses 64 gives its lowest bits */
+    uint32_t take = 0u;
+    if (inc <= 64u) {
+        take = w;
+    } else if (inc - pc < 64u) {
+        for (uint32_t k = 64u - (inc - pc), rest = w; k; k--) {
+            take |= rest & (0u - rest);
+            rest &= rest - 1u;
+        }
+    }
+    const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
+    const uint32_t ng = __builtin_popcount(got);
+    uint32_t off = ng;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(off, d, 64);
+        if (lane >= (uint32_t)d) off += o;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(off, 63);
+    off -= ng;
+    for (uint32_t b = got; b; b &= b - 1u) sh->stage[wave][off++] = (uint16_t)(lane * 32u + __builtin_ctz(b));
+    if (lane == 0 && total) atomicSub(&sh->count[best], total);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
+    *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
+    return total;
+}
 
 #ifdef DPRF_R6_TIMING
-/* debug builds (-DDPRF_R6_TIMING): per-wave cycle split of the round loop, printed for a few workgroups */
-#define R6T_DECL unsigned long long t_bar = 0, t_fam = 0, t_work = 0, t_x = __builtin_readcyclecounter(); \
-    unsigned long long t_cyc[2] = {0, 0}, t_units[2] = {0, 0}, t_nb[2] = {0, 0};
+/* debug builds (-DDPRF_R6_TIMING): per-wave cycles in rounds vs waiting for queued slots */
+#define R6T_DECL unsigned long long t_work = 0, t_wait = 0, t_x = __builtin_readcyclecounter(), t_nb = 0, t_part = 0;
 #define R6T_MARK(acc) { unsigned long long t_y = __builtin_readcyclecounter(); acc += t_y - t_x; t_x = t_y; }
 #else
 #define R6T_DECL
@@ -406,102 +465,47 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     uint8_t *cs = (uint8_t *)smem;                                              /* 256 B */
     r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
     const uint32_t patbase = lds_addr(smem) + 256u + (uint32_t)((sizeof(r6_shared) + 15) / 16 * 16);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, nthr = blockDim.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nthr = blockDim.x;
     /* Te0 copies into bytes 0..127 of each row; the upper halves are slot periods */
     for (uint32_t k = tid; k < 256u * R6_TE_COPIES; k += nthr)
         r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = T->te0[k >> 5];
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
-    if (tid < 8) sh->hist[tid] = 0u;
+    for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
+    if (tid < R6_CLASSES) sh->count[tid] = 0u;
+    if (tid == 0) sh->live = 0u;
     __syncthreads();
 
-    for (uint32_t sl = tid; sl < nslots; sl += nthr)
-        r6_start<MODE>(e, p, cs, R, stop_on_first, sh, slot_lds(patbase, pat_words, te_slots, sl, lane), sl);
+    for (uint32_t sl = tid; sl < nslots; sl += nthr) {
+        const r6_lds S = slot_lds(patbase, pat_words, te_slots, sl, lane);
+        if (r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, sl)) {
+            atomicAdd(&sh->live, 1u);
+            r6_push(sh, S, sl);
+        }
+    }
+    __syncthreads();
     R6T_DECL
+    uint32_t idle = 0;
     for (;;) {
-        R6T_MARK(t_work)
-        __syncthreads();
-        R6T_MARK(t_bar)
-        /* 1. family of each slot this thread looks after; rank within its class by an LDS atomic */
-        uint32_t mycls[R6_SLOTS_PER_THREAD], myrank[R6_SLOTS_PER_THREAD], myh[R6_SLOTS_PER_THREAD];
-#pragma unroll
-        for (int q = 0; q < R6_SLOTS_PER_THREAD; q++) {
-            const uint32_t sl = tid + (uint32_t)q * nthr;
-            mycls[q] = R6_CLASSES - 1; myh[q] = 0; myrank[q] = 0;
-            if (sl < nslots) {
-                if (sh->cand[sl] != R6_IDLE) {
-                    const uint32_t st = sh->state[sl];
-                    myh[q] = r6_family(slot_lds(patbase, pat_words, te_slots, sl, lane), st & 0xffu);
-                    mycls[q] = (myh[q] ? 3u : 0u) + (((st >> 8) & 0xffu) - 32u) / 16u;
-                }
-                myrank[q] = atomicAdd(&sh->hist[mycls[q]], 1u);
+        uint32_t slot;
+        const uint32_t n = r6_claim(sh, lane, wave, &slot);
+        if (n == 0) {
+            if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
+            /* watchdog: a wave that has found nothing queued for ~1 s of sleeps (a round takes ~1 ms) gives
+             * up and flags the launch instead of hanging the device; the host turns the flag into an error */
+            if (++idle > (1u << 22)) {
+                if (lane == 0) atomicOr(&R->pad_, 1u);
+                break;
             }
+            __builtin_amdgcn_s_sleep(4);
+            R6T_MARK(t_wait)
+            continue;
         }
-        R6T_MARK(t_fam)
-        __syncthreads();
-        R6T_MARK(t_bar)
-        if (sh->hist[R6_CLASSES - 1] == nslots) break;             /* no slot has a candidate: uniform exit */
-#pragma unroll
-        for (int q = 0; q < R6_SLOTS_PER_THREAD; q++) {
-            const uint32_t sl = tid + (uint32_t)q * nthr;
-            if (sl < nslots) {
-                uint32_t pos = myrank[q];
-#pragma unroll
-                for (uint32_t k = 0; k < R6_CLASSES - 1; k++) pos += k < mycls[q] ? sh->hist[k] : 0u;
-                sh->order[pos] = (uint16_t)sl;
-                sh->state[sl] |= myh[q] << 30;          /* round counter (bits 16..29) < 2^14 */
-            }
-        }
-        /* 2. batches of 64 within each family group, longest-processing-time-first onto the waves */
-        if (tid == 0) {
-            uint32_t nb = 0, base = 0;
-            for (uint32_t fg = 0; fg < 2; fg++) {
-                uint32_t n = sh->hist[3 * fg] + sh->hist[3 * fg + 1] + sh->hist[3 * fg + 2];
-                for (uint32_t o = 0; o < n; o += 64u) {
-                    const uint32_t sz = n - o < 64u ? n - o : 64u;
-                    /* longest period of the batch: its last slot (sorted by bs within the family) */
-                    const uint32_t stl = sh->state[sh->order[base + o + sz - 1]];
-                    sh->bstart[nb] = (uint16_t)(base + o);
-                    sh->bsize[nb] = (uint8_t)sz;
-                    sh->bcost[nb] = r6_cost(fg, (stl & 0xffu) + ((stl >> 8) & 0xffu));
-                    nb++;
-                }
-                base += n;
-            }
-            /* sort batch ids by cost, descending (insertion sort, <= 22 entries) */
-            for (uint32_t b = 0; b < nb; b++) {
-                uint32_t k = b;
-                const uint32_t cb = sh->bcost[b];
-                while (k > 0 && sh->bcost[sh->ids[k - 1]] < cb) { sh->ids[k] = sh->ids[k - 1]; k--; }
-                sh->ids[k] = (uint8_t)b;
-            }
-            sh->nbatches = nb;
-            sh->next_batch = 0;
-        }
-        __syncthreads();
-        if (tid < 8) sh->hist[tid] = 0u;
-        /* 3. rounds of batches, costliest first, each wave taking the next one when it is free */
-        const uint32_t nb = sh->nbatches;
-        for (;;) {
-            /* the wave takes the costliest batch nobody has taken yet (greedy list scheduling in
-             * cost order: waves that run faster -- fewer co-resident waves on their SIMD -- take more) */
-            uint32_t kk = 0;
-            if (lane == 0) kk = atomicAdd(&sh->next_batch, 1u);
-            kk = __builtin_amdgcn_readfirstlane(kk);
-            if (kk >= nb) break;
-            const uint32_t b = sh->ids[kk];
+        idle = 0;
 #ifdef DPRF_R6_TIMING
-            const unsigned long long tb0 = __builtin_readcyclecounter();
-            if (lane == 0) {
-                const uint32_t stl = sh->state[sh->order[sh->bstart[b] + sh->bsize[b] - 1]];
-                t_units[stl >> 30 ? 1 : 0] += (stl & 0xffu) + ((stl >> 8) & 0xffu);
-                t_nb[stl >> 30 ? 1 : 0] += 1;
-            }
-            struct tb_guard { unsigned long long t0, *acc; uint32_t on;
-                __device__ ~tb_guard() { if (on) *acc += __builtin_readcyclecounter() - t0; } };
-            tb_guard tg{tb0, &t_cyc[sh->state[sh->order[sh->bstart[b] + sh->bsize[b] - 1]] >> 30 ? 1 : 0], lane == 0};
+        t_nb++;
+        t_part += n;
 #endif
-            if (lane >= sh->bsize[b]) continue;
-            const uint32_t slot = sh->order[sh->bstart[b] + lane];
+        if (slot != R6_IDLE) {
             const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, lane);
             const uint32_t st = sh->state[slot];
             const uint32_t len = st & 0xffu, hs = st >> 30;
@@ -509,6 +513,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             uint32_t K[16];
             const uint32_t last = r6_round(S, len, bs, hs, K);
             i++;
+            bool more = true;
             if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
                 bool ok = true;
 #pragma unroll
@@ -520,16 +525,19 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     atomicMin(&R->first, idx);
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
-                r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
+                more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot);
+                if (!more) atomicSub(&sh->live, 1u);
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);
             }
+            if (more) r6_push(sh, S, slot);
         }
+        R6T_MARK(t_work)
     }
 #ifdef DPRF_R6_TIMING
     if (lane == 0 && blockIdx.x < 2)
-        printf("r6 timing wg %u wave %u: work %llu fam %llu barrier %llu | sha256 batches %llu units %llu cyc %llu | sha512 batches %llu units %llu cyc %llu\n",
-               blockIdx.x, tid >> 6, t_work, t_fam, t_bar, t_nb[0], t_units[0], t_cyc[0], t_nb[1], t_units[1], t_cyc[1]);
+        printf("r6 timing wg %u wave %u: work %llu wait %llu batches %llu slots %llu\n", blockIdx.x, wave, t_work,
+               t_wait, t_nb, t_part);
 #endif
 }
 

@@ -31,7 +31,7 @@ struct dprf_results {
     uint32_t nhits;                 /* total hits (may exceed cap) */
     uint32_t stop;                  /* set by a hit when stop_on_first */
     uint32_t cursor;                /* work cursor of persistent kernels (PDF R6), reset per launch */
-    uint32_t pad_;
+    uint32_t pad_;                  /* error flags set by a kernel (PDF R6 scheduler watchdog), 0 = none */
     unsigned long long first;       /* lowest hit index (atomicMin), ~0 if none */
     unsigned long long skipped;     /* candidates of launched chunks NOT evaluated: stop_on_first blocks
                                        skipped above the lowest hit (rare: one atomic per skipped block, none
