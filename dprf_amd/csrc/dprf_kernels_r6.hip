@@ -128,27 +128,39 @@ DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const ui
 /* Load candidate `idx` (keyspace index or slot), compute K = SHA256(pw || salt), write pw to the
  * head of the lane's pattern column.  Returns the password length. */
 template <int MODE>
-DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, uint64_t idx,
-                       const r6_lds &S, uint32_t K[16]) {
+DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, const uint8_t *sdig,
+                       uint64_t idx, const r6_lds &S, uint32_t K[16]) {
     uint32_t w[DPRF_SLOT_WORDS];
 #pragma unroll
     for (int j = 0; j < DPRF_SLOT_WORDS; j++) w[j] = 0;
     uint32_t len;
     if (MODE == 0) {
+        /* a runtime loop over the pwlen positions (uniform), each character stored straight into the slot's
+         * period column and the words read back: unrolled over DPRF_MAX_RANGE_LEN with the digits and the
+         * words in registers, this once-per-candidate code spilled 300 B per lane in every wave of the
+         * kernel (~2 KB of scratch writes per candidate, profiles/pmc_traffic.json r01) */
         uint32_t rem = (uint32_t)(idx - e.start), carry = 0;
-#pragma unroll
-        for (int pp = DPRF_MAX_RANGE_LEN - 1; pp >= 0; --pp) {
-            if ((uint32_t)pp < e.pwlen) {
-                uint32_t q = e.cslen == 1 ? rem : fastdiv6(rem, e.div_m, e.div_s);
-                uint32_t r = rem - q * e.cslen;
-                uint32_t d = (uint32_t)e.sdig[pp] + r + carry;
-                carry = d >= e.cslen ? 1u : 0u;
-                d -= carry ? e.cslen : 0u;
-                rem = q;
-                w[pp >> 2] |= (uint32_t)cs[d] << (8 * (pp & 3));
-            }
+        const uint32_t n = e.pwlen;
+#pragma unroll 1
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t pp = n - 1u - k;
+            const uint32_t q = e.cslen == 1 ? rem : fastdiv6(rem, e.div_m, e.div_s);
+            const uint32_t r = rem - q * e.cslen;
+            uint32_t d = (uint32_t)sdig[pp] + r + carry;      /* LDS copy: a runtime index into the byval
+                                                                 kernel argument would put it on the stack */
+            carry = d >= e.cslen ? 1u : 0u;
+            d -= carry ? e.cslen : 0u;
+            rem = q;
+            *L8(S.pat + pat_addr(pp, S.lanebase)) = cs[d];
         }
-        len = e.pwlen;
+        len = n;
+        /* opaque per-lane length: with the launch-uniform pwlen visible, LLVM hoists this once-per-candidate
+         * SHA-256's uniform message words and K+W sums out of the persistent loop into ~70 long-lived VGPRs,
+         * which then spill (~280 B per lane of scratch) */
+        asm volatile("" : "+v"(len));
+#pragma unroll
+        for (int j = 0; j < DPRF_SLOT_WORDS; j++)
+            w[j] = 4u * (uint32_t)j < len ? *L32(S.pat + (((uint32_t)j << 8) | S.lanebase)) : 0u;
     } else {
         const uint4 *s = (const uint4 *)(e.slots + idx * DPRF_SLOT_WORDS);
 #pragma unroll
@@ -345,6 +357,7 @@ struct r6_shared {
     uint32_t count[R6_CLASSES];               /* queued slots per class (a hint for picking the class) */
     uint32_t live;                            /* slots holding a candidate                             */
     uint32_t nslots, te_slots, pad;
+    uint8_t sdig[DPRF_MAX_RANGE_LEN];         /* base-cslen digits of the launch's first index          */
     uint16_t stage[R6_LANES / 64][64];        /* per wave: the slot ids of the batch it claimed         */
     uint32_t state[R6_MAX_SLOTS];             /* len | bs << 8 | round << 16                            */
     uint32_t cand[R6_MAX_SLOTS];              /* candidate offset within the launch, R6_IDLE when none  */
@@ -380,7 +393,7 @@ DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
     sh->cand[slot] = c;
     if (c == R6_IDLE) return false;
     uint32_t K[16];
-    const uint32_t len = r6_begin<MODE>(e, p, cs, e.start + c, S, K);
+    const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, e.start + c, S, K);
     r6_store_k(S, len, 32u, K);
     sh->state[slot] = len | (32u << 8);
     return true;
@@ -472,6 +485,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
     if (tid < R6_CLASSES) sh->count[tid] = 0u;
+    if (tid < DPRF_MAX_RANGE_LEN) sh->sdig[tid] = e.sdig[tid];
     if (tid == 0) sh->live = 0u;
     __syncthreads();
 
