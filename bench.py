@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU candidates per step (default per workload)")
     ap.add_argument("--no-side", action="store_true", help="skip the per-format side measurements")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--no-cluster", action="store_true", help="skip the configs[4] server + GPU client leg")
+    ap.add_argument("--cluster-candidates", type=int, default=12 << 20)
     ap.add_argument("--stop-on-first", action="store_true",
                     help="time the product's early-stop rounds instead of full verification of every batch")
     args = ap.parse_args()
@@ -391,6 +393,20 @@ def main():
                 side[name]["cpu_baseline"] = side_cpu[name]
             sctx.close()
 
+    cluster = None
+    if rank == 0 and n_gpus == 1 and not args.no_side and not args.no_cluster:
+        # configs[4]: server + GPU clients over TCP on this box (2 client processes on this GPU hide each
+        # other's request/parse gaps), Office test document, -pr 8 order, 2^20-candidate payloads
+        sys.path.insert(0, os.path.join(HERE, "tools"))
+        import bench_cluster
+        try:
+            cluster = bench_cluster.run(gpus=1, clients_per_gpu=2, payload=1 << 20,
+                                        candidates=args.cluster_candidates, workload="office",
+                                        timeout=180, devices=[local])
+            cluster.pop("clients_detail", None)
+        except Exception as ex:   # the leg is reported, never fatal to the headline line
+            cluster = {"error": repr(ex)}
+
     if rank == 0:
         roof = {"bound": work.BOUND.get(wkey, "valu"), "achieved": m["achieved"] / 1e12, "peak": peak / 1e12,
                 "unit": "T VALU lane-slots/s (gfx950 issue-slot floor of the algorithm)",
@@ -430,6 +446,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "per_format": side,
+            "cluster": cluster,
             "lowest_hit_index": None if lowest is None or lowest >= (1 << 62) else lowest,
         }
         print(json.dumps(out), flush=True)

@@ -29,6 +29,56 @@ def free_port():
     return p
 
 
+def run(gpus=1, clients_per_gpu=2, payload=1 << 20, candidates=24 << 20, workload="office", builders=4,
+        timeout=300, dry_run=False, devices=None):
+    """Start the server and the clients, wait for the server to drain; returns the result dict."""
+    stream = json.load(open(os.path.join(REPO, "tests", "golden", "streams.json")))[DOCS[workload]]["stream"]
+    port, hb = free_port(), free_port()
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+    srv = subprocess.Popen([sys.executable, "-m", "dprf_amd.server", "1", "unused.docx", "-pr", "8", "-ps",
+                            str(payload), "127.0.0.1", str(port), "--stream", stream, "--max-candidates",
+                            str(candidates), "--heartbeat-port", str(hb), "--quiet", "--builders",
+                            str(builders)], cwd=REPO, env=env, stdout=subprocess.PIPE, text=True)
+    for _ in range(100):                       # wait for the work port
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.2).close()
+            break
+        except OSError:
+            time.sleep(0.1)
+    # (the server ignores the empty probe connection)
+    clients = []
+    for g in (devices if devices is not None else range(gpus)):
+        for _ in range(clients_per_gpu):
+            cenv = dict(env)
+            cenv["HIP_VISIBLE_DEVICES"] = str(g)
+            clients.append(subprocess.Popen([sys.executable, "-m", "dprf_amd.client", "127.0.0.1", str(port),
+                                             "--devices", "0", "--quiet", "--heartbeat-port", str(hb)]
+                                            + (["--dry-run"] if dry_run else []),
+                                            cwd=REPO, env=cenv, stdout=subprocess.PIPE, text=True))
+    t0 = time.time()
+    try:
+        out, _ = srv.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        srv.kill()
+        for c in clients:
+            c.kill()
+        raise
+    res = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    couts = []
+    for c in clients:
+        o, _ = c.communicate(timeout=60)
+        couts += [json.loads(l) for l in o.splitlines() if l.startswith("{")]
+    s = res[-1] if res else {}
+    return {"metric": "end-to-end verified candidates/sec, server.py + GPU client.py (configs[4])"
+                      + (" -- DRY RUN: clients verify nothing" if dry_run else ""),
+            "workload": workload, "n_gpus": gpus, "clients": len(clients), "payload": payload,
+            "candidates": s.get("acknowledged"), "value": s.get("rate"), "unit": "candidates/s",
+            "server_from_first_payload_s": s.get("from_first_payload_s"),
+            "client_verified": sum(c["verified"] for c in couts),
+            "clients_detail": couts, "wall_s": time.time() - t0, "complete": s.get("acknowledged") == candidates}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -40,48 +90,10 @@ def main():
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--dry-run", action="store_true", help="clients parse payloads but verify nothing (no GPU)")
     args = ap.parse_args()
-
-    stream = json.load(open(os.path.join(REPO, "tests", "golden", "streams.json")))[DOCS[args.workload]]["stream"]
-    port, hb = free_port(), free_port()
-    env = dict(os.environ)
-    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
-    srv = subprocess.Popen([sys.executable, "-m", "dprf_amd.server", "1", "unused.docx", "-pr", "8", "-ps",
-                            str(args.payload), "127.0.0.1", str(port), "--stream", stream, "--max-candidates",
-                            str(args.candidates), "--heartbeat-port", str(hb), "--quiet", "--builders",
-                            str(args.builders)], cwd=REPO, env=env, stdout=subprocess.PIPE, text=True)
-    for _ in range(100):                       # wait for the work port
-        try:
-            socket.create_connection(("127.0.0.1", port), timeout=0.2).close()
-            break
-        except OSError:
-            time.sleep(0.1)
-    # (the server ignores the empty probe connection)
-    clients = []
-    for g in range(args.gpus):
-        for _ in range(args.clients_per_gpu):
-            cenv = dict(env)
-            cenv["HIP_VISIBLE_DEVICES"] = str(g)
-            clients.append(subprocess.Popen([sys.executable, "-m", "dprf_amd.client", "127.0.0.1", str(port),
-                                             "--devices", "0", "--quiet", "--heartbeat-port", str(hb)]
-                                            + (["--dry-run"] if args.dry_run else []),
-                                            cwd=REPO, env=cenv, stdout=subprocess.PIPE, text=True))
-    t0 = time.time()
-    out, _ = srv.communicate(timeout=args.timeout)
-    res = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
-    couts = []
-    for c in clients:
-        o, _ = c.communicate(timeout=60)
-        couts += [json.loads(l) for l in o.splitlines() if l.startswith("{")]
-    s = res[-1] if res else {}
-    line = {"metric": "end-to-end verified candidates/sec, server.py + GPU client.py (configs[4])"
-                      + (" -- DRY RUN: clients verify nothing" if args.dry_run else ""),
-            "workload": args.workload, "n_gpus": args.gpus, "clients": len(clients), "payload": args.payload,
-            "candidates": s.get("acknowledged"), "value": s.get("rate"), "unit": "candidates/s",
-            "server_from_first_payload_s": s.get("from_first_payload_s"),
-            "client_verified": sum(c["verified"] for c in couts),
-            "clients_detail": couts, "wall_s": time.time() - t0}
+    line = run(args.gpus, args.clients_per_gpu, args.payload, args.candidates, args.workload, args.builders,
+               args.timeout, args.dry_run)
     print(json.dumps(line), flush=True)
-    return 0 if s.get("acknowledged") == args.candidates else 1
+    return 0 if line["complete"] else 1
 
 
 if __name__ == "__main__":
