@@ -617,49 +617,9 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     lds_st8(S, (63u << 8) + 3u + lanebase, px);
 }
 
-/* One-step-ahead KSA schedule, used for R2 (one KSA per candidate).  Step i issues its S[j_i] read and
- * the S[i+1] prefetch BEFORE the two swap writes of step i-1, so the reads return memory as of step i-2
- * and are repaired in registers:
- *   S[j_i]  after steps <= i-1 = (j_i == j_{i-1}) ? s_{i-1} : (j_i == i-1) ? sj_{i-1} : read
- *   S[i+1]  after steps <= i   = (j_i == i+1) ? s_i : (j_{i-1} == i+1) ? s_{i-1} : read
- * (step i-1 writes S[i-1] = sj_{i-1} first, then S[j_{i-1}] = s_{i-1}, so the latter wins on a tie).
- * A/B on one box (tools/ab_r24.sh, bench.py pdf_r2): 4.98 G cand/s with this schedule and a full 32-byte
- * PRGA, 4.50 G with the grouped KSA below, 4.77 G with this one plus the 2-byte early reject -- for one
- * KSA per candidate the extra code and the reject branch cost more than they save. */
-template <int NK>
-DEVI void rc4_ksa_ahead(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
-#pragma unroll
-    for (int w = 0; w < 64; w++) *(uint32_t *)(S + (w << 8) + lanebase) = 0x03020100u + 0x04040404u * (uint32_t)w;
-    uint32_t kb[NK];
-#pragma unroll
-    for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
-    uint32_t j = 0, s_cur = 0, pj = 0, ps = 0, psj = 0;
-#pragma unroll
-    for (int i = 0; i < 256; i++) {
-        const uint32_t ji = (j + s_cur + kb[i % NK]) & 0xffu;
-        const uint32_t aj = rc4_addr(ji, lanebase);
-        uint32_t x = lds_ld8(S, aj);
-        uint32_t y = 0;
-        if (i < 255) y = lds_ld8(S, ((uint32_t)((i + 1) >> 2) << 8) + (uint32_t)((i + 1) & 3) + lanebase);
-        if (i > 0) {
-            lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, psj);
-            lds_st8(S, rc4_addr(pj, lanebase), ps);
-            x = (ji == pj) ? ps : ((ji == (uint32_t)(i - 1)) ? psj : x);
-        }
-        const uint32_t sj = x;
-        if (i < 255) {
-            uint32_t nxt = y;
-            if (i > 0) nxt = (pj == (uint32_t)(i + 1)) ? ps : nxt;
-            nxt = (ji == (uint32_t)(i + 1)) ? s_cur : nxt;
-            pj = ji; ps = s_cur; psj = sj; s_cur = nxt;
-        } else {
-            pj = ji; ps = s_cur; psj = sj;
-        }
-        j = ji;
-    }
-    lds_st8(S, (63u << 8) + 3u + lanebase, psj);
-    lds_st8(S, rc4_addr(pj, lanebase), ps);
-}
+/* R2 used a one-step-ahead KSA (S[j] and S[i+1] read before the previous step's two stores, both repaired
+ * in registers) until round 2: re-measured after the SDWA address and the 4-byte PRGA reject, the grouped
+ * deferred-store rc4_ksa above is 23 % faster for R2 too (6.67 -> 8.20 G cand/s, tools/ab_libs.sh). */
 /* PRGA of NB bytes XORed into d[] (LE-packed). */
 /* PRGA bytes FROM..TO (1-based keystream positions), j carried in and out, XORed into d[] (LE-packed) */
 template <int FROM, int TO>
@@ -842,7 +802,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             uint32_t d[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-            rc4_ksa_ahead<5>(Sw, lanebase, h);
+            rc4_ksa<5>(Sw, lanebase, h);
 #ifndef DPRF_R2_FULL_PRGA
             /* the first 4 keystream bytes decide for all but a 2^-32 fraction of the lanes: the wave
              * continues the same keystream (i = 5.., j carried) only when one of its lanes matches U[0:4] */

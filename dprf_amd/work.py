@@ -136,12 +136,12 @@ BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "lds", "pd
 #   R3/R4 (rc4_ksa, k_pdf_r24): identity 64 x addtid (128) + 256 steps x (S[j] read 2 + S[j] and S[i]
 #   stores 8) + 63 dword reads of the next S[i] group (126) = 2,814 per KSA; the 2-byte PRGA of the
 #   early-reject pass 5 reads + 2 stores = 18; 20 passes.
-#   R2 (rc4_ksa_ahead): identity 64 x ds_write_b32 (256) + 256 x (S[j] and S[i+1] reads 4 + 2 stores 8)
-#   - the last S[i+1] read (2) + 4 PRGA bytes x (3 reads + 2 stores = 14) (the other 28 bytes only in the
-#   2^-32 of waves where a lane matches U[0:4]).
+#   R2 (the same grouped rc4_ksa since round 2): identity 64 x addtid (128) + 256 x 10 + 63 dword reads
+#   (126) + 4 PRGA bytes x (3 reads + 2 stores = 14) (the other 28 bytes only in the 2^-32 of waves where a
+#   lane matches U[0:4]).
 LDS_CYCLES = {
     "pdf_r34": 20 * (128 + 256 * 10 + 63 * 2 + 18) / 64.0,
-    "pdf_r2": (256 + 256 * 12 - 2 + 4 * 14) / 64.0,
+    "pdf_r2": (128 + 256 * 10 + 63 * 2 + 4 * 14) / 64.0,
 }
 PEAK_LDS_CYCLES_PER_S = 256 * 2.4e9          # one LDS per CU
 

@@ -63,7 +63,7 @@ def test_lds_cycle_model():
     # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (2 + 4 + 4) + 63 dword reads x 2 + PRGA-2: 5 x 2 + 2 x 4)
     assert work.LDS_CYCLES["pdf_r34"] * 64 == 20 * (64 * 2 + 256 * 10 + 63 * 2 + 5 * 2 + 2 * 4)
     # R2: 64 ds_write_b32 x 4 + 256 x (2 reads + 2 stores) - last S[i+1] read + 4 x (3 reads + 2 stores)
-    assert work.LDS_CYCLES["pdf_r2"] * 64 == 64 * 4 + 256 * (2 * 2 + 2 * 4) - 2 + 4 * (3 * 2 + 2 * 4)
+    assert work.LDS_CYCLES["pdf_r2"] * 64 == 64 * 2 + 256 * 10 + 63 * 2 + 4 * (3 * 2 + 2 * 4)
     assert work.lds_frac("odt", 1e6) is None
     assert abs(work.lds_frac("pdf_r34", 1e6) - 1e6 * work.LDS_CYCLES["pdf_r34"] / (256 * 2.4e9)) < 1e-12
     for fmt in work.LDS_CYCLES:
