@@ -195,3 +195,91 @@ def test_gpu_client_against_server(streams):
         th.join(10)
         assert (rc, pw) == (0, d["password"]), name
         assert out["pw"] == d["password"]
+
+
+class _FakeCtx:
+    """Stand-in for _lib.Context on CPU (test infrastructure): the oracle's verdicts, and the library's
+    list-mode rule that one invalid candidate fails the whole call (dprf_verify_list) while
+    dprf_list_status marks it."""
+
+    def __init__(self, fields, devices=None):
+        import pyoracle
+        self.c = pyoracle.Ctx(fields)
+        self.devices = devices
+
+    def _status(self, p):
+        from dprf_amd import _lib
+        if b"\x00" in p:
+            return _lib.E_INVALID
+        if not p:
+            return _lib.E_DOMAIN
+        return _lib.E_PWLEN if len(p.decode("utf-8", "replace").encode("utf-16-le")) > 64 else 0
+
+    def list_status(self, blob, offsets):
+        b = bytes(blob)
+        return np.array([self._status(b[int(offsets[k]):int(offsets[k + 1])]) for k in range(len(offsets) - 1)],
+                        dtype=np.int8)
+
+    def verify_blob(self, blob, offsets, stop_on_first=False, cap=1 << 16):
+        from dprf_amd import _lib
+        st = self.list_status(blob, offsets)
+        if (st != 0).any():
+            k = int(np.flatnonzero(st)[0])
+            raise _lib.DprfError(int(st[k]), "candidate %d invalid" % k)
+        b = bytes(blob)
+        hits = [k for k in range(len(offsets) - 1) if self.c.verify(b[int(offsets[k]):int(offsets[k + 1])])]
+        return hits[:cap], len(hits), {}
+
+    def close(self):
+        pass
+
+
+def test_gpu_verifier_drops_invalid_candidates_instead_of_failing(streams, monkeypatch):
+    """a payload with a candidate the format cannot take (NUL, empty Office password, > 32 UTF-16
+    units) is verified without it -- the reference fails such a candidate in its own process -- rather than
+    crashing every client it is re-queued to.  The lowest VALID index that verifies is the answer."""
+    from dprf_amd import _lib
+    monkeypatch.setattr(_lib, "Context", _FakeCtx)
+    s = streams["office_testdoc"]["stream"]
+    ver = cl.GpuVerifier(devices=[0])
+    pws = ["x", "", "bad\x00nul", "y" * 40, "password", "password"]
+    blob, offs = pl._pack(pws)
+    assert ver(s, blob, offs) == (1, "password")
+    assert ver.skipped == 3 and ver.verified == len(pws)
+    blob, offs = pl._pack(["a", "b"])
+    assert ver(s, blob, offs) == (0, None)          # the valid-only path leaves clean payloads alone
+    ver.close()
+
+
+def test_server_survives_a_client_that_dies_before_reading(streams):
+    """sendall to a client that is gone must not end the server; the payload stays for the next
+    connection."""
+    srv = sv.Server(streams["office_testdoc"]["stream"], password_range=2, payload_size=50, quiet=True,
+                    heartbeat_port=0)
+    msg, segs = srv.prepare_data_for_transfer()
+
+    class Once:
+        """A client socket that sends its request, then is gone before the answer."""
+
+        def recv(self, n):
+            if getattr(self, "done", False):
+                return b""
+            self.done = True
+            return json.dumps({"found": False, "correct_password": "", "id": "c1"}).encode()
+
+        def settimeout(self, t):
+            pass
+
+        def shutdown(self, how):
+            pass
+
+        def sendall(self, m):
+            raise BrokenPipeError("client went away")
+
+        def close(self):
+            pass
+
+    found, sent = srv.handle_connection(Once(), ("127.0.0.1", 1), msg, segs)
+    assert (found, sent) == (False, False)
+    assert srv.clients == [] and "c1" not in srv.processed_passwords
+    srv.pool.shutdown(wait=False)
