@@ -319,11 +319,23 @@ static int parse_pdf(dprf_ctx *c, const char *const *f) {
 /* Candidates per launch.  A device takes its next chunk from the call's shared cursor sized for about
  * `target_ms` of device time at the rate it measured on its last launch (`init` before the first), a
  * power of two in [lo, hi].  The floors keep whole waves of workgroups on the chip: Office's 2^19 is one
- * full generation of k_office_kdf (256 CUs x 32 waves x 64 lanes); R6's persistent workgroups need ~8
- * candidates per slot per launch to amortise the round-length tail. */
+ * full generation of k_office_kdf (256 CUs x 32 waves x 64 lanes); R6's persistent workgroups drain at the
+ * end of every launch, so its launches take ~3 s (below). */
 struct chunk_policy { uint32_t init, lo, hi; double target_ms; };
 #ifndef DPRF_R24_HI_LOG2
 #define DPRF_R24_HI_LOG2 30
+#endif
+/* R6: every launch of the persistent kernel ends in a drain (the last candidates' ~35 remaining rounds with
+ * fewer live slots than lanes), so its launches are long: same 2^23-candidate steps measured 2.79 / 2.92 /
+ * 3.00 M cand/s with 2^21 / 2^22 / 2^23 per launch (tools/ab_r6_chunk.sh, round 2) */
+#ifndef DPRF_R6_LO_LOG2
+#define DPRF_R6_LO_LOG2 21
+#endif
+#ifndef DPRF_R6_HI_LOG2
+#define DPRF_R6_HI_LOG2 24
+#endif
+#ifndef DPRF_R6_TARGET_MS
+#define DPRF_R6_TARGET_MS 3000.0
 #endif
 static chunk_policy policy(kernel_kind k) {
     switch (k) {
@@ -331,7 +343,7 @@ static chunk_policy policy(kernel_kind k) {
         case K_ODT: return {1u << 22, 1u << 19, 1u << 23, 300.0};
         case K_PDF_R24: return {1u << 24, 1u << 20, 1u << DPRF_R24_HI_LOG2, 100.0};
         case K_PDF_R5: return {1u << 27, 1u << 22, 1u << 31, 100.0};
-        case K_PDF_R6: return {1u << 21, 1u << 20, 1u << 22, 1000.0};
+        case K_PDF_R6: return {1u << 22, 1u << DPRF_R6_LO_LOG2, 1u << DPRF_R6_HI_LOG2, DPRF_R6_TARGET_MS};
         default: return {1u << 24, 1u << 20, 1u << 24, 100.0};
     }
 }

@@ -251,8 +251,14 @@ DEVI uint32_t r6_family(const r6_lds &S, uint32_t len) {
 
 /* One round of the hardened hash for a slot whose family `hsel` is known: returns E[last]; K (16 BE
  * words, zero past the digest) and bs become the next round's; K[0:bs] is stored back into the period. */
+/* UNI (range mode): every slot of a batch has the same period length (fixed pwlen, one bs per class) and
+ * every batch one family, so Lp, the block offset o and the byte selector are wave-uniform scalars and a
+ * block's LDS address is one v_add of the lane's column base (~15 VALU slots per AES block saved). */
+template <bool UNI>
 DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16]) {
-    const uint32_t Lp = len + bs;
+    uint32_t Lp = len + bs;
+    if (UNI) Lp = __builtin_amdgcn_readfirstlane(Lp);
+    const uint32_t colbase = S.pat + S.lanebase;                 /* pat is only 16-byte aligned */
     r6_load_k(S, len, K);
     /* AES-128 key K[0:16], iv K[16:32] (:259-261) */
     uint32_t rk[44];
@@ -273,7 +279,17 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             uint32_t v[4], y[4];
-            r6_read16(S, o, v);
+            if (UNI) {
+                const uint32_t sel = 0x00010203u + (o & 3u) * 0x01010101u;
+                const lds_u32 *col = L32(colbase + ((o >> 2) << 8));
+                uint32_t lw[5];
+#pragma unroll
+                for (int k = 0; k < 5; k++) lw[k] = col[k * 64];
+#pragma unroll
+                for (int k = 0; k < 4; k++) v[k] = perm(lw[k + 1], lw[k], sel);
+            } else {
+                r6_read16(S, o, v);
+            }
             aes128_encrypt_te(S, rk, v[0] ^ prev[0], v[1] ^ prev[1], v[2] ^ prev[2], v[3] ^ prev[3], y);
 #pragma unroll
             for (int k = 0; k < 4; k++) { prev[k] = y[k]; w[4 * q + k] = y[k]; }
@@ -525,7 +541,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             const uint32_t len = st & 0xffu, hs = st >> 30;
             uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
             uint32_t K[16];
-            const uint32_t last = r6_round(S, len, bs, hs, K);
+            const uint32_t last = r6_round<MODE == 0>(S, len, bs, hs, K);
             i++;
             bool more = true;
             if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
