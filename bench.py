@@ -298,12 +298,18 @@ def main():
     import torch
     from dprf_amd import _lib, brute_force, work
 
+    # Rehearsal knobs for the N>1 path on a 1-GPU box (never used by the driver): DPRF_BENCH_SAME_DEVICE=1
+    # puts every rank on device 0 and DPRF_BENCH_BACKEND=gloo exchanges through CPU tensors (RCCL refuses two
+    # ranks on one GPU).  The driver's runs use one GPU per rank and RCCL.
+    backend = os.environ.get("DPRF_BENCH_BACKEND", "nccl")
+    if os.environ.get("DPRF_BENCH_SAME_DEVICE") == "1":
+        local = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     # one process per GPU under torchrun (world = N); `--gpus N` without a launcher drives N GPUs from this
     # one process through one multi-device library context instead
     devices = [local]
@@ -313,7 +319,7 @@ def main():
             raise SystemExit("--gpus %d: only %d gfx950 devices visible" % (args.gpus, len(devices)))
 
     def sync():
-        for d in devices:
+        for d in sorted(set(devices)):
             torch.cuda.synchronize(torch.device("cuda", d))
         if dist:
             dist.barrier()
