@@ -554,6 +554,90 @@ static double run(int blocks, int reps, uint32_t *dout, std::vector<uint32_t> &h
     return ms / reps;
 }
 
+
+/* Round 2: two KSAs (passes 2x and 2x+1 of one candidate: their keystreams are independent, RC4(k,c) = c ^ ks)
+ * interleaved step by step in one wave, variant-9 schedule each, S-boxes in two 16 KiB halves of a 32 KiB
+ * block: 4 waves/CU instead of 9, but every wave carries two independent j chains (in-wave ILP instead of
+ * cross-wave latency hiding). */
+DEVI void ksa9x2(uint8_t *SA, uint8_t *SB, uint32_t lanebase, const uint32_t kA[4], const uint32_t kB[4]) {
+    sbox_init(SA, lanebase);
+    sbox_init(SB, lanebase);
+    uint32_t kbA[16], kbB[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        kbA[q] = (kA[q >> 2] >> (8 * (q & 3))) & 0xffu;
+        kbB[q] = (kB[q >> 2] >> (8 * (q & 3))) & 0xffu;
+    }
+    uint32_t jA = 0, jB = 0, WA = 0x03020100u, WB = 0x03020100u, pxA = 0, pxB = 0;
+#pragma unroll
+    for (int q = 0; q < 64; q++) {
+        const uint32_t base = 4u * (uint32_t)q;
+        uint32_t sA[4], mA[4], sB[4], mB[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = 4 * q + r;
+            uint32_t vA = __builtin_amdgcn_ubfe(WA, 8 * r, 8), vB = __builtin_amdgcn_ubfe(WB, 8 * r, 8);
+#pragma unroll
+            for (int rr = 0; rr < r; rr++) {
+                vA = (mA[rr] == base + (uint32_t)r) ? sA[rr] : vA;
+                vB = (mB[rr] == base + (uint32_t)r) ? sB[rr] : vB;
+            }
+            sA[r] = vA; sB[r] = vB;
+            jA = jA + vA + kbA[i & 15]; jB = jB + vB + kbB[i & 15];
+            mA[r] = jA & 0xffu; mB[r] = jB & 0xffu;
+            const uint32_t aA = rc4_addr_sdwa(jA, lanebase), aB = rc4_addr_sdwa(jB, lanebase);
+            uint32_t xA = ld8(SA, aA), xB = ld8(SB, aB);
+            if (i > 0) {
+                st8(SA, posaddr(i - 1, lanebase), pxA);
+                st8(SB, posaddr(i - 1, lanebase), pxB);
+                xA = (mA[r] == (uint32_t)(i - 1)) ? pxA : xA;
+                xB = (mB[r] == (uint32_t)(i - 1)) ? pxB : xB;
+            }
+            st8(SA, aA, vA);
+            st8(SB, aB, vB);
+            pxA = xA; pxB = xB;
+        }
+        if (q < 63) {
+            WA = *(const uint32_t *)(SA + ((q + 1) << 8) + lanebase);
+            WB = *(const uint32_t *)(SB + ((q + 1) << 8) + lanebase);
+        }
+    }
+    st8(SA, posaddr(255, lanebase), pxA);
+    st8(SB, posaddr(255, lanebase), pxB);
+}
+
+__global__ void __launch_bounds__(64) k_rc4_x2(uint32_t *out) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[32768];
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t lanebase = threadIdx.x << 2;
+    uint32_t h[4] = {mix(g), mix(g + 0x9e3779b9u), mix(g ^ 0x5bd1e995u), mix(g * 3u + 1u)};
+    uint32_t d[4] = {0x11111111u, 0x22222222u, 0x33333333u, 0x44444444u};
+    for (uint32_t x = 0; x < 20u; x += 2) {
+        const uint32_t xa = x * 0x01010101u, xb = (x + 1) * 0x01010101u;
+        uint32_t ka[4] = {h[0] ^ xa, h[1] ^ xa, h[2] ^ xa, h[3] ^ xa};
+        uint32_t kb2[4] = {h[0] ^ xb, h[1] ^ xb, h[2] ^ xb, h[3] ^ xb};
+        ksa9x2(S, S + 16384, lanebase, ka, kb2);
+        prga16(S, lanebase, d);
+        prga16(S + 16384, lanebase, d);
+    }
+    out[4 * g + 0] = d[0]; out[4 * g + 1] = d[1]; out[4 * g + 2] = d[2]; out[4 * g + 3] = d[3];
+}
+
+static double run_x2(int blocks, int reps, uint32_t *dout, std::vector<uint32_t> &host) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
+    hipLaunchKernelGGL(k_rc4_x2, dim3(blocks), dim3(64), 0, 0, dout);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a, 0));
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k_rc4_x2, dim3(blocks), dim3(64), 0, 0, dout);
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipMemcpy(host.data(), dout, host.size() * 4, hipMemcpyDeviceToHost));
+    return ms / reps;
+}
+
 int main(int argc, char **argv) {
     const int blocks = argc > 1 ? atoi(argv[1]) : 65536;
     const int reps = argc > 2 ? atoi(argv[2]) : 5;
@@ -572,6 +656,11 @@ int main(int argc, char **argv) {
 #define VAR(V) ms[V] = run<V>(blocks, reps, dout, got); if (got != ref) { printf("variant %d MISMATCH\n", V); bad = 1; }
     VAR(1) VAR(2) VAR(3) VAR(4) VAR(5) VAR(6) VAR(7) VAR(8) VAR(9)
     ms[10] = run<10>(blocks, reps, dout, got); ms[11] = run<11>(blocks, reps, dout, got); ms[12] = run<12>(blocks, reps, dout, got);
+    {
+        const double mx2 = run_x2(blocks, reps, dout, got);
+        if (got != ref) { printf("variant x2 MISMATCH\n"); bad = 1; }
+        printf("variant x2 (two interleaved KSAs per wave, 32 KiB): %.3f ms -> %.1f M cand/s\n", mx2, n / mx2 / 1e3);
+    }
     for (int v = 0; v < 13; v++)
         printf("variant %d: %.3f ms / launch of %zu lanes -> %.1f M cand/s (20 x KSA+PRGA16)\n", v, ms[v], n,
                n / ms[v] / 1e3);
