@@ -536,8 +536,9 @@ template <class MK>
 static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_result &out) {
     char buf[600];
     auto hip_fail = [&](const char *what, hipError_t e) {
-        snprintf(buf, sizeof buf, "%s (device %d): %s", what, L.device, hipGetErrorString(e));
-        cs.error(DPRF_E_HIP, buf);
+        char msg[700];   /* `what` may be buf itself */
+        snprintf(msg, sizeof msg, "%s (device %d): %s", what, L.device, hipGetErrorString(e));
+        cs.error(DPRF_E_HIP, msg);
     };
     hipError_t e = hipSetDevice(L.device);
     if (e != hipSuccess) { hip_fail("hipSetDevice", e); return; }
