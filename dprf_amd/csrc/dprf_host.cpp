@@ -563,7 +563,9 @@ static void lane_run(dprf_ctx *c, dev_lane &L, call_state &cs, MK &mk, lane_resu
         out.launches++;
         const unsigned long long f = L.h_ring[s].first;
         if (f != ~0ull) atomic_min_u64(cs.first, f);
-        else if (ms > 0.05f) L.rate = nchunk[s] / (double)ms;   /* a launch with no skipped blocks */
+        /* the launch's rate (candidates / device ms) sizes this device's next chunks; a launch may have
+         * skipped blocks only with stop_on_first after a hit */
+        if ((!cs.stop_on_first || f == ~0ull) && ms > 0.05f) L.rate = nchunk[s] / (double)ms;
         head = (head + 1) % DEPTH;
         inq--;
         return hipSuccess;
