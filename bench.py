@@ -395,6 +395,9 @@ def main():
             pc = pmc_summary(name)
             if pc:
                 side[name]["rocprof"] = pc
+            tr = json.load(open(pmc)).get(name, {}) if os.path.exists(pmc) else {}
+            if tr:
+                side[name]["traffic_bytes_per_launch"] = tr.get("bytes_per_launch")
             if name in side_cpu:
                 side[name]["cpu_baseline"] = side_cpu[name]
             sctx.close()
