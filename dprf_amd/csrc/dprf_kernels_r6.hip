@@ -367,6 +367,9 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #define R6_CLASSES 6
 #define R6_MAP_WORDS ((R6_MAX_SLOTS + 31) / 32)
 #define R6_IDLE 0xffffffffu
+#ifndef R6_WATCHDOG_S
+#define R6_WATCHDOG_S 10u           /* seconds a wave may find nothing queued while slots are live */
+#endif
 
 struct r6_shared {
     uint32_t map[R6_CLASSES][R6_MAP_WORDS];   /* queued slots of each class, one bit per slot          */
@@ -489,7 +492,7 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
 template <int MODE>
 __global__ void __launch_bounds__(R6_LANES, 1)     /* 12 waves/CU: <= 168 VGPRs */
 k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
-         uint32_t stop_on_first, uint32_t pat_words, uint32_t nslots, uint32_t te_slots) {
+         uint32_t stop_on_first, uint32_t pat_words, uint32_t nslots, uint32_t te_slots, uint64_t idle_ticks) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];               /* after r6_te */
     uint8_t *cs = (uint8_t *)smem;                                              /* 256 B */
     r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
@@ -514,15 +517,21 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     }
     __syncthreads();
     R6T_DECL
-    uint32_t idle = 0;
+    bool idling = false;
+    uint64_t idle_t0 = 0;
     for (;;) {
         uint32_t slot;
         const uint32_t n = r6_claim(sh, lane, wave, &slot);
         if (n == 0) {
             if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
-            /* watchdog: a wave that has found nothing queued for ~1 s of sleeps (a round takes ~1 ms) gives
-             * up and flags the launch instead of hanging the device; the host turns the flag into an error */
-            if (++idle > (1u << 22)) {
+            /* watchdog on the constant-rate wall clock: a wave that has found nothing queued for idle_ticks
+             * (host: 10 s; a whole launch is ~3 s and the drain after the cursor runs dry tens of ms) gives up
+             * and flags the launch instead of hanging the device; the host turns the flag into an error */
+            const uint64_t now = wall_clock64();
+            if (!idling) {
+                idling = true;
+                idle_t0 = now;
+            } else if (now - idle_t0 > idle_ticks) {
                 if (lane == 0) atomicOr(&R->pad_, 1u);
                 break;
             }
@@ -530,7 +539,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             R6T_MARK(t_wait)
             continue;
         }
-        idle = 0;
+        idling = false;
 #ifdef DPRF_R6_TIMING
         t_nb++;
         t_part += n;
@@ -611,6 +620,10 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     if (dev < 0 || dev >= R6_MAX_DEVICES) return hipErrorInvalidDevice;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
+    int clk_khz = 0;                                              /* wall_clock64() rate (100 MHz on gfx9) */
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, dev);
+    if (clk_khz <= 0) clk_khz = 100000;
+    const uint64_t idle_ticks = (uint64_t)clk_khz * 1000u * R6_WATCHDOG_S;
     /* one workgroup per CU; a launch smaller than the slots it would open uses fewer workgroups */
     uint32_t grid = (e.count + nslots - 1) / nslots;
     if (grid > (uint32_t)ncu) grid = (uint32_t)ncu;
@@ -627,8 +640,10 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
         }
     }
     if (e.mode == 0)
-        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
+        hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots,
+                           te_slots, idle_ticks);
     else
-        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots, te_slots);
+        hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots,
+                           te_slots, idle_ticks);
     return hipGetLastError();
 }
