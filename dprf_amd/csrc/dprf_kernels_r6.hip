@@ -14,9 +14,9 @@
  *    its own LDS bank column ([word][lane], so a lane's words share one bank) and pulls each 16-byte
  *    block out of it with 5 ds_read_b32 + 4 v_perm; ciphertext goes straight into the SHA message
  *    registers 64 bytes (4 AES blocks) at a time.
- *  - AES T-table: Te0 only (Te1..3 by rotation), replicated 16x across banks (entry x of copy c at
- *    word 16x+c, lane l reads copy l%16) -- random table indices otherwise pile up on few banks
- *    (measured 1.5x, tools/aes_lds_bench.hip).  The last round takes S[x] from byte 2 of Te0[x].
+ *  - AES T-tables: Te0 and Te2 = ror16(Te0), each replicated 16x across banks (lane l reads copy l%16);
+ *    a round column is Te0[a] ^ Te2[c] ^ ror8(Te0[b] ^ Te2[d] ^ rol8 k), one rotate instead of three.
+ *    The last round takes S[x] from byte 2 of Te0[x].
  *  - Persistent lanes: a wave owns a contiguous range of candidates; a lane that finishes its
  *    candidate (after 64..~110 rounds) immediately takes the next one, so the wave never idles on its
  *    slowest lane until the range is exhausted.
@@ -29,13 +29,21 @@
 
 #include <mutex>
 
-/* Te0 replicated 32x: entry x, copy c at byte 256*x + 4*c (c < 32).  Lane l reads copy l%32, so each
- * 32-lane group of a ds_read_b32 ({0-31}, {32-63}: MI355X_MICROARCH.md LDS table) hits 32 different banks
- * whatever the indices (conflict-free), and the address of byte k of a state word is ONE v_perm: byte 1
- * <- byte k of the word, byte 0 <- 4*(lane%32), bytes 2-3 <- 0.  Bytes 128..255 of every row are free:
- * they hold the periods of 32-slot groups (slot_lds), so the 64 KiB the addressing needs is not lost. */
+/* T-tables in bytes 0..127 of 256-byte rows, row x = entry x: R6_TABLES tables (table t = ror(Te0, 8t), or
+ * Te2 = ror16(Te0) as the second of two), each replicated 32/R6_TABLES times; copy c of table t at byte
+ * 256*x + 4*(c + t*copies), lane l reads copy l%copies.  The address of byte k of a state word is ONE
+ * v_perm: byte 1 <- byte k of the word, byte 0 <- 4*(lane%copies), bytes 2-3 <- 0 (+ the table's offset
+ * as an immediate).  Bytes 128..255 of every row are free: they hold the periods of 32-slot groups
+ * (slot_lds), so the 64 KiB the addressing needs is not lost.
+ * Two tables (default): a 32-lane group of a ds_read_b32 ({0-31}, {32-63}: MI355X_MICROARCH.md LDS table)
+ * meets each of 16 banks twice (2-way conflicts) but a column needs one rotate instead of three --
+ * 3.02 -> 3.18 M cand/s over one table × 32 copies (conflict-free); four tables × 8 copies (no rotates,
+ * 4-way conflicts): 1.91 M.  (round 2, tools/ab_libs.sh pdf_r6) */
 #define R6_TE_ROW_BYTES 256
-#define R6_TE_COPIES 32
+#ifndef R6_TABLES
+#define R6_TABLES 2
+#endif
+#define R6_TE_COPIES (32 / R6_TABLES)
 #define R6_TE_BYTES (256 * R6_TE_ROW_BYTES)
 
 DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
@@ -57,7 +65,7 @@ DEVI uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(const lds_u8 *
 struct r6_lds {
     uint32_t pat;              /* LDS byte address of the slot's group: rows of 256 bytes */
     uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
-    uint32_t lanec;            /* 4 * (thread lane % 32): this thread's Te0 copy */
+    uint32_t lanec;            /* 4 * (thread lane % R6_TE_COPIES): this thread's table copy */
 };
 
 /* Te0[byte k of v] */
@@ -65,6 +73,12 @@ template <int K>
 DEVI uint32_t teb(const r6_lds &S, uint32_t v) {
     const uint32_t a = __builtin_amdgcn_perm(v, S.lanec, 0x0c0c0000u | ((4u + K) << 8));
     return *(const uint32_t *)((const uint8_t *)r6_te + a);
+}
+/* table T (ror(Te0, 8T), or ror16 for T = 1 of two tables) [byte k of v]: its copies follow table T-1's */
+template <int T, int K>
+DEVI uint32_t tebt(const r6_lds &S, uint32_t v) {
+    const uint32_t a = __builtin_amdgcn_perm(v, S.lanec, 0x0c0c0000u | ((4u + K) << 8));
+    return *(const uint32_t *)((const uint8_t *)r6_te + 4 * R6_TE_COPIES * T + a);
 }
 DEVI uint32_t pat_addr(uint32_t pos, uint32_t lanebase) { return ((pos >> 2) << 8) | (pos & 3u) | lanebase; }
 
@@ -83,6 +97,11 @@ DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[4
         rk[4 * i + 6] = rk[4 * i + 2] ^ rk[4 * i + 5];
         rk[4 * i + 7] = rk[4 * i + 3] ^ rk[4 * i + 6];
     }
+#if R6_TABLES == 2
+    /* the inner rounds add their key inside the ror8 of the two-table column: store it rotated back */
+#pragma unroll
+    for (int i = 4; i < 40; i++) rk[i] = ror32(rk[i], 24);
+#endif
 }
 
 DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0, uint32_t s1, uint32_t s2,
@@ -90,6 +109,18 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 10; r++) {
+#if R6_TABLES == 4
+        const uint32_t t0 = xor3(xor3(teb<3>(S, s0), tebt<1, 2>(S, s1), tebt<2, 1>(S, s2)), tebt<3, 0>(S, s3), rk[4 * r]);
+        const uint32_t t1 = xor3(xor3(teb<3>(S, s1), tebt<1, 2>(S, s2), tebt<2, 1>(S, s3)), tebt<3, 0>(S, s0), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(teb<3>(S, s2), tebt<1, 2>(S, s3), tebt<2, 1>(S, s0)), tebt<3, 0>(S, s1), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(teb<3>(S, s3), tebt<1, 2>(S, s0), tebt<2, 1>(S, s1)), tebt<3, 0>(S, s2), rk[4 * r + 3]);
+#elif R6_TABLES == 2
+        /* Te0[a] ^ ror8 Te0[b] ^ ror16 Te0[c] ^ ror24 Te0[d] ^ k = Te0[a] ^ Te2[c] ^ ror8(Te0[b] ^ Te2[d] ^ rol8 k) */
+        const uint32_t t0 = xor3(teb<3>(S, s0), tebt<1, 1>(S, s2), ror32(xor3(teb<2>(S, s1), tebt<1, 0>(S, s3), rk[4 * r]), 8));
+        const uint32_t t1 = xor3(teb<3>(S, s1), tebt<1, 1>(S, s3), ror32(xor3(teb<2>(S, s2), tebt<1, 0>(S, s0), rk[4 * r + 1]), 8));
+        const uint32_t t2 = xor3(teb<3>(S, s2), tebt<1, 1>(S, s0), ror32(xor3(teb<2>(S, s3), tebt<1, 0>(S, s1), rk[4 * r + 2]), 8));
+        const uint32_t t3 = xor3(teb<3>(S, s3), tebt<1, 1>(S, s1), ror32(xor3(teb<2>(S, s0), tebt<1, 0>(S, s2), rk[4 * r + 3]), 8));
+#else
         const uint32_t t0 = xor3(xor3(teb<3>(S, s0), ror32(teb<2>(S, s1), 8), ror32(teb<1>(S, s2), 16)),
                                  ror32(teb<0>(S, s3), 24), rk[4 * r]);
         const uint32_t t1 = xor3(xor3(teb<3>(S, s1), ror32(teb<2>(S, s2), 8), ror32(teb<1>(S, s3), 16)),
@@ -98,6 +129,7 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
                                  ror32(teb<0>(S, s1), 24), rk[4 * r + 2]);
         const uint32_t t3 = xor3(xor3(teb<3>(S, s3), ror32(teb<2>(S, s0), 8), ror32(teb<1>(S, s1), 16)),
                                  ror32(teb<0>(S, s2), 24), rk[4 * r + 3]);
+#endif
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     /* last round: SubBytes + ShiftRows + AddRoundKey, S[x] = byte 2 of Te0[x] */
@@ -392,7 +424,7 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
         S.pat = patbase + (t >> 6) * pat_words * 256u;
         S.lanebase = (t & 63u) << 2;
     }
-    S.lanec = (lane & 31u) << 2;
+    S.lanec = (lane & (R6_TE_COPIES - 1u)) << 2;
     return S;
 }
 
@@ -499,8 +531,11 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     const uint32_t patbase = lds_addr(smem) + 256u + (uint32_t)((sizeof(r6_shared) + 15) / 16 * 16);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nthr = blockDim.x;
     /* Te0 copies into bytes 0..127 of each row; the upper halves are slot periods */
-    for (uint32_t k = tid; k < 256u * R6_TE_COPIES; k += nthr)
-        r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = T->te0[k >> 5];
+    /* the tables' copies fill bytes 0..127 of each row: table t = ror(Te0, 8t) (16t with two tables) */
+    for (uint32_t k = tid; k < 256u * 32u; k += nthr) {
+        const uint32_t t = (k & 31u) / R6_TE_COPIES;
+        r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = ror32(T->te0[k >> 5], (R6_TABLES == 2 ? 16 : 8) * t);
+    }
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
     if (tid < R6_CLASSES) sh->count[tid] = 0u;
