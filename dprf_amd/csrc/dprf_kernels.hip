@@ -526,12 +526,9 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
  * these 16 KiB (charset, PAD and the stop flag are overlaid on the S-box area before the first KSA), so
  * 10 one-wave workgroups fit a CU's 160 KiB. */
 #define RC4_WAVE_BYTES 16384
-DEVI uint32_t rc4_addr(uint32_t j, uint32_t lanebase) {
-    return ((__builtin_amdgcn_ubfe(j, 2, 6)) << 8) | (j & 3u) | lanebase;
-}
-/* rc4_addr in two half-rate instructions: (j & 3) | lanebase, then byte 1 <- (j & 0xff) >> 2 by an SDWA shift
- * that keeps the other bytes (lanebase < 256).  tools/rc4_bench.hip variant 9: +3.6% on the R3/R4 KSA; the
- * R2 kernel (one KSA per candidate, ahead schedule) measured 6% slower with it, so it keeps rc4_addr. */
+/* Address of S[j & 0xff] = ((j & 0xfc) << 6) | (j & 3) | lanebase in two half-rate instructions: (j & 3) | lanebase, then byte 1 <- (j & 0xff) >> 2 by an SDWA shift
+ * that keeps the other bytes (lanebase < 256); any j (only its low byte counts).  tools/rc4_bench.hip
+ * variant 9: +3.6% on the R3/R4 KSA.  Used by every KSA and PRGA step. */
 DEVI uint32_t rc4_addr_sdwa(uint32_t j, uint32_t lanebase) {
     uint32_t t = (j & 3u) | lanebase;
     asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
@@ -575,21 +572,25 @@ DEVI void rc4_identity(uint8_t *S) {
  * of the group swapped into that position (S[j] = s with j = 4q+r; a compare-select per earlier step).
  * So the j chain waits on LDS once per four steps.  Every step still reads S[j] and stores both sides of
  * the swap in program order, so LDS is current for every position -- except that the S[i] = S[j] store
- * is issued one step late (after the next step's S[j] read, which is repaired when it hits i), so the
- * wave does not stall on its own read right after issuing it.
- * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs): this
- * schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a register and stored
- * once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain 334 M.  At 16 KiB per
- * wave only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
+ * is issued one step late, after the next step's S[j] read (which missed it when it hit i), and the value
+ * it stores -- that read's result, repaired -- is only formed then too: the wave waits for a read one step
+ * old instead of the one it has just issued.
+ * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs, round 1): the
+ * deferred-store schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a register
+ * and stored once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain 334 M.  In the
+ * product (round 2, tools/ab_libs.sh): repairing the read one step late, 443.7 -> 456 M (R3/R4) and
+ * 8.19 -> 8.47 G (R2); byte compares on j itself (v_cmp_eq_u32_sdwa src0_sel:BYTE_0, no j & 0xff) 464 M /
+ * 8.70 G.  At 16 KiB per wave only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     rc4_identity(S);
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
-    uint32_t j = 0;
+    uint32_t j = 0;                             /* only its low byte is meaningful */
     uint32_t W = 0x03020100u;                   /* dword 0 is the identity */
-    uint32_t px = 0;                            /* S[i-1] value whose store is deferred */
+    uint32_t px = 0;                            /* S[i-2] value (repaired), stored at step i-1 */
+    uint32_t xr = 0, pm = 0xffffffffu;          /* the previous step's raw S[j] read and its j & 0xff */
 #pragma unroll
     for (int q = 0; q < 64; q++) {
         const uint32_t base = 4u * (uint32_t)q;
@@ -602,25 +603,29 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
             s[r] = v;
             j = j + v + kb[i % NK];
+            /* used only in compares, which LLVM folds into SDWA byte selects of j (the address asm takes
+             * byte 0 of j itself, so nothing needs the masked value) */
             m[r] = j & 0xffu;
-            const uint32_t a = rc4_addr_sdwa(m[r], lanebase);
-            uint32_t x = lds_ld8(S, a);
+            const uint32_t a = rc4_addr_sdwa(j, lanebase);
+            const uint32_t x = lds_ld8(S, a);
             if (i > 0) {
-                lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, px);
-                x = (m[r] == (uint32_t)(i - 1)) ? px : x;
+                /* the previous step's read missed the store of S[i-2] (issued after it) when it hit i-2 */
+                const uint32_t pv = (pm == (uint32_t)(i - 2)) ? px : xr;
+                lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, pv);
+                px = pv;
             }
             lds_st8(S, a, v);
-            px = x;
+            xr = x;
+            pm = m[r];
         }
         if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
     }
-    lds_st8(S, (63u << 8) + 3u + lanebase, px);
+    lds_st8(S, (63u << 8) + 3u + lanebase, (pm == 254u) ? px : xr);
 }
 
 /* R2 used a one-step-ahead KSA (S[j] and S[i+1] read before the previous step's two stores, both repaired
  * in registers) until round 2: re-measured after the SDWA address and the 4-byte PRGA reject, the grouped
  * deferred-store rc4_ksa above is 23 % faster for R2 too (6.67 -> 8.20 G cand/s, tools/ab_libs.sh). */
-/* PRGA of NB bytes XORed into d[] (LE-packed). */
 /* PRGA bytes FROM..TO (1-based keystream positions), j carried in and out, XORed into d[] (LE-packed) */
 template <int FROM, int TO>
 DEVI void rc4_prga_span(uint8_t *S, uint32_t lanebase, uint32_t d[], uint32_t &j) {
@@ -629,11 +634,11 @@ DEVI void rc4_prga_span(uint8_t *S, uint32_t lanebase, uint32_t d[], uint32_t &j
         const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
         const uint32_t si = lds_ld8(S, ai);
         j = j + si;
-        const uint32_t aj = rc4_addr(j, lanebase);
+        const uint32_t aj = rc4_addr_sdwa(j, lanebase);
         const uint32_t sj = lds_ld8(S, aj);
         lds_st8(S, ai, sj);
         lds_st8(S, aj, si);
-        const uint32_t ks = lds_ld8(S, rc4_addr(si + sj, lanebase));
+        const uint32_t ks = lds_ld8(S, rc4_addr_sdwa(si + sj, lanebase));
         d[(i - 1) >> 2] ^= ks << (8 * ((i - 1) & 3));
     }
 }
@@ -645,11 +650,11 @@ DEVI void rc4_prga(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
         const uint32_t ai = ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase;
         const uint32_t si = lds_ld8(S, ai);
         j = j + si;
-        const uint32_t aj = rc4_addr(j, lanebase);
+        const uint32_t aj = rc4_addr_sdwa(j, lanebase);
         const uint32_t sj = lds_ld8(S, aj);
         lds_st8(S, ai, sj);
         lds_st8(S, aj, si);
-        const uint32_t ks = lds_ld8(S, rc4_addr(si + sj, lanebase));
+        const uint32_t ks = lds_ld8(S, rc4_addr_sdwa(si + sj, lanebase));
         d[(i - 1) >> 2] ^= ks << (8 * ((i - 1) & 3));
     }
 }
@@ -663,18 +668,18 @@ DEVI void rc4_prga<2>(uint8_t *S, uint32_t lanebase, uint32_t d[]) {
     const uint32_t a1 = (0u << 8) + 1u + lanebase;
     const uint32_t s1 = lds_ld8(S, a1);
     j = s1 & 0xffu;
-    const uint32_t aj1 = rc4_addr(j, lanebase);
+    const uint32_t aj1 = rc4_addr_sdwa(j, lanebase);
     const uint32_t sj1 = lds_ld8(S, aj1);
     lds_st8(S, a1, sj1);
     lds_st8(S, aj1, s1);
-    const uint32_t k1 = lds_ld8(S, rc4_addr(s1 + sj1, lanebase));
+    const uint32_t k1 = lds_ld8(S, rc4_addr_sdwa(s1 + sj1, lanebase));
     /* byte 2: reads after byte 1's swap (in order); its own swap is applied in registers */
     const uint32_t a2 = 2u + lanebase;
     const uint32_t s2 = lds_ld8(S, a2);
     const uint32_t j2 = (j + s2) & 0xffu;
-    const uint32_t sj2 = lds_ld8(S, rc4_addr(j2, lanebase));
+    const uint32_t sj2 = lds_ld8(S, rc4_addr_sdwa(j2, lanebase));
     const uint32_t t = (s2 + sj2) & 0xffu;
-    uint32_t k2 = lds_ld8(S, rc4_addr(t, lanebase));
+    uint32_t k2 = lds_ld8(S, rc4_addr_sdwa(t, lanebase));
     k2 = (t == j2) ? s2 : ((t == 2u) ? sj2 : k2);
     d[0] ^= k1 | (k2 << 8);
 }
