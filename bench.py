@@ -251,6 +251,18 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
     return dt, stats, lowest, pwlen
 
 
+def launch_traffic(path, workload, per_launch):
+    """HBM bytes (FETCH_SIZE + WRITE_SIZE) of the dominant kernel per launch of THIS run: the profile's bytes
+    per candidate x this run's candidates per launch (the adaptive chunking may size launches differently
+    from the profiled run); the profiled per-launch figure when the summary predates per-candidate bytes."""
+    if not os.path.exists(path):
+        return None
+    tr = json.load(open(path)).get(workload, {})
+    if tr.get("bytes_per_candidate") is not None and per_launch:
+        return tr["bytes_per_candidate"] * per_launch
+    return tr.get("bytes_per_launch")
+
+
 def pmc_summary(workload):
     """rocprof-derived counters of the workload's dominant kernel (profiles/pmc_valu.json, written by
     tools/pmc_valu.py from the tools/profile_gpu.sh passes): VALUBusy, VALUUtilization, LDS busy."""
@@ -366,10 +378,8 @@ def main():
     dt_max = allreduce_max(dt)
     m = summarize(stats, wkey, world, dt_max)
     peak = work.PEAK_LANE_INSTR_PER_S
-    traffic = None
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get(args.workload, {}).get("bytes_per_launch")
+    traffic = launch_traffic(pmc, args.workload, m["per_launch"])
     counters = pmc_summary(args.workload)
 
     side = {}
@@ -395,9 +405,9 @@ def main():
             pc = pmc_summary(name)
             if pc:
                 side[name]["rocprof"] = pc
-            tr = json.load(open(pmc)).get(name, {}) if os.path.exists(pmc) else {}
-            if tr:
-                side[name]["traffic_bytes_per_launch"] = tr.get("bytes_per_launch")
+            tr = launch_traffic(pmc, name, sm["per_launch"])
+            if tr is not None:
+                side[name]["traffic_bytes_per_launch"] = tr
             if name in side_cpu:
                 side[name]["cpu_baseline"] = side_cpu[name]
             sctx.close()

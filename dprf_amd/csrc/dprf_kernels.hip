@@ -580,7 +580,12 @@ DEVI void rc4_identity(uint8_t *S) {
  * and stored once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain 334 M.  In the
  * product (round 2, tools/ab_libs.sh): repairing the read one step late, 443.7 -> 456 M (R3/R4) and
  * 8.19 -> 8.47 G (R2); byte compares on j itself (v_cmp_eq_u32_sdwa src0_sel:BYTE_0, no j & 0xff) 464 M /
- * 8.70 G.  At 16 KiB per wave only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
+ * 8.70 G.  LLVM still hoists some repairs right after the read they wait on; forcing every wait onto the
+ * previous step's read was slower (asm pin 461 M; __builtin_amdgcn_sched_barrier 442 M; a software-pipelined
+ * order that waits on the read two steps back 445 M, 452 M without barriers; storing S[i] two steps late
+ * 434 M; no deferral at all 405 M): the VALU chain and the LDS issue rate (~10.5 LDS cycles per step, 67 %
+ * busy), not the read latency, bound the loop now.  At 16 KiB per wave only 9 waves fit a CU
+ * (tools/lds_occ.hip: <= 15,360 B gives 10). */
 template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     rc4_identity(S);

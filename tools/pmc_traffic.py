@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Collect the dominant kernel's PMC figures from the profile summaries (tools/prof_summary.py output):
-  profiles/pmc_traffic.json  HBM bytes per launch (FETCH_SIZE + WRITE_SIZE) -> bench.py roofline.traffic
+  profiles/pmc_traffic.json  HBM bytes per candidate and per profiled launch (FETCH_SIZE + WRITE_SIZE) ->
+                             bench.py roofline.traffic (per candidate x bench's own candidates per launch)
   profiles/pmc_valu.json     VALUBusy, VALUUtilization, LDS busy, effective clock -> bench.py roofline.valu_busy
 
 FETCH_SIZE / WRITE_SIZE come from separate rocprofv3 --pmc passes (they cannot share one on gfx950) and are
@@ -32,6 +33,7 @@ for w, kname in DOM.items():
         src = os.path.relpath(f, HERE)
         if v.get("hbm_bytes_per_dispatch") is not None:
             traffic[w] = {"kernel": k, "bytes_per_launch": v.get("hbm_bytes_per_dispatch"),
+                          "bytes_per_candidate": v.get("hbm_bytes_per_candidate"),
                           "fetch_bytes": pd.get("FETCH_SIZE", 0) * 1024, "write_bytes": pd.get("WRITE_SIZE", 0) * 1024,
                           "source": src}
         if v.get("valu_busy") is not None:

@@ -10,6 +10,10 @@ each kernel, and the derived metrics are computed within one pass:
   valu_utilization = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)           (ROCm's VALUUtilization)
   lds_busy         = SQ_ACTIVE_INST_LDS * 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs)    (same form, LDS instructions)
   effective_clock  = GRBM_GUI_ACTIVE / XCDs / kernel duration
+HBM bytes are also given per candidate (each PMC pass runs bench.py --steps 1 --warmup 0, i.e. exactly one
+batch of candidates, whatever launch sizes the adaptive chunking chose), so bench.py can scale them to its own
+launch size; and the kernel-trace pass reports the mean duration of the dominant kernel over the TIMED
+dispatches only (the last steps x launches-per-step), the figure bench.py's roofline.kernel_avg_ms measures.
 """
 import collections
 import csv
@@ -20,6 +24,26 @@ import sys
 
 SIMDS, XCDS = 256 * 4, 8
 PASSES = ("fetch", "write", "sq", "lds")
+PMC_STEPS = 1          # tools/profile_gpu.sh: --steps 1 --warmup 0 for every --pmc pass
+
+
+def timed_dispatches(src, bench):
+    """Mean duration of the dominant kernel over the timed dispatches of the kernel-trace pass."""
+    f = os.path.join(src, "kt", "kt_kernel_trace.csv")
+    roof = (bench or {}).get("roofline") or {}
+    if not os.path.exists(f) or not roof.get("candidates_per_launch"):
+        return None
+    rows = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0]
+        if not k.startswith("__amd"):
+            rows[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    dom = max(rows, key=lambda k: sum(d for _, d in rows[k]))
+    per_step = max(1, round(bench["config"]["batch_per_gpu"] / roof["candidates_per_launch"]))
+    n = per_step * bench["steps"]
+    durs = [d for _, d in sorted(rows[dom])][-n:]
+    return {"kernel": dom, "dispatches": len(durs), "avg_ns": sum(durs) / len(durs),
+            "all_dispatches": len(rows[dom]), "all_avg_ns": sum(d for _, d in rows[dom]) / len(rows[dom])}
 
 
 def summarize(src, dst):
@@ -35,6 +59,11 @@ def summarize(src, dst):
             out["bench_under_profiler"] = json.load(open(bench))
         except ValueError:
             pass
+    bp = out.get("bench_under_profiler")
+    t = timed_dispatches(src, bp)
+    if t:
+        out["timed_kernel"] = t
+    batch = ((bp or {}).get("config") or {}).get("batch_per_gpu")
     # kernel -> pass -> counter -> {dispatch: value}
     raw = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(dict)))
     dur = collections.defaultdict(lambda: collections.defaultdict(dict))
@@ -56,6 +85,7 @@ def summarize(src, dst):
             avg = {name: sum(v.values()) / len(v) for name, v in ctrs.items()}
             ns = sum(dur[k][sub].values()) / max(1, len(dur[k][sub]))
             per["passes"][sub] = dict(avg, kernel_ns=ns, dispatches=len(dur[k][sub]))
+            per.setdefault("per_run_total", {}).update({name: sum(v.values()) for name, v in ctrs.items()})
             per["per_dispatch"].update(avg)
             g = avg.get("GRBM_GUI_ACTIVE")
             if g:
@@ -74,6 +104,11 @@ def summarize(src, dst):
             # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads 1/2 of wide streaming
             # reads (MI355X_MICROARCH.md HBM section) -- these kernels have no streaming reads, no correction.
             per["hbm_bytes_per_dispatch"] = (pd.get("FETCH_SIZE", 0) + pd.get("WRITE_SIZE", 0)) * 1024
+            if batch:
+                tot = per["per_run_total"]
+                per["pmc_candidates"] = batch * PMC_STEPS
+                per["hbm_bytes_per_candidate"] = (tot.get("FETCH_SIZE", 0) + tot.get("WRITE_SIZE", 0)) * 1024 / (
+                    batch * PMC_STEPS)
         summ[k] = per
     out["counters"] = summ
     json.dump(out, open(dst + ".json", "w"), indent=1)
