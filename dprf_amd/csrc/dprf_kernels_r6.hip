@@ -89,9 +89,14 @@ DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[4
 #pragma unroll
     for (int i = 0; i < 10; i++) {
         const uint32_t t = rk[4 * i + 3];
+#if R6_TABLES == 2
+        /* SubWord(RotWord(t)): S[x] in bytes 3, 0 of Te2[x] and 2, 1 of Te0[x] (see the last round) */
+        const uint32_t sw = perm(tebt<1, 2>(S, t), teb<1>(S, t), 0x07020c0cu) | perm(teb<0>(S, t), tebt<1, 3>(S, t), 0x0c0c0500u);
+#else
         /* SubWord(RotWord(t)) with S[x] = byte 2 of Te0[x] */
         const uint32_t sw = ((teb<2>(S, t) << 8) & 0xff000000u) | (teb<1>(S, t) & 0x00ff0000u) |
                             ((teb<0>(S, t) >> 8) & 0x0000ff00u) | ((teb<3>(S, t) >> 16) & 0xffu);
+#endif
         rk[4 * i + 4] = rk[4 * i] ^ sw ^ rcon[i];
         rk[4 * i + 5] = rk[4 * i + 1] ^ rk[4 * i + 4];
         rk[4 * i + 6] = rk[4 * i + 2] ^ rk[4 * i + 5];
@@ -132,6 +137,18 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
 #endif
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
+#if R6_TABLES == 2
+    /* last round: SubBytes + ShiftRows + AddRoundKey.  S[x] sits in bytes 2 and 1 of Te0[x] and in bytes 3
+     * and 0 of Te2[x], i.e. already where each output byte needs it: two v_perm and one or-xor per word */
+    {
+        const uint32_t HI = 0x07020c0cu, LO = 0x0c0c0500u;   /* src0.b3 src1.b2 0 0 | 0 0 src0.b1 src1.b0 */
+        out[0] = (perm(tebt<1, 3>(S, s0), teb<2>(S, s1), HI) | perm(teb<1>(S, s2), tebt<1, 0>(S, s3), LO)) ^ rk[40];
+        out[1] = (perm(tebt<1, 3>(S, s1), teb<2>(S, s2), HI) | perm(teb<1>(S, s3), tebt<1, 0>(S, s0), LO)) ^ rk[41];
+        out[2] = (perm(tebt<1, 3>(S, s2), teb<2>(S, s3), HI) | perm(teb<1>(S, s0), tebt<1, 0>(S, s1), LO)) ^ rk[42];
+        out[3] = (perm(tebt<1, 3>(S, s3), teb<2>(S, s0), HI) | perm(teb<1>(S, s1), tebt<1, 0>(S, s2), LO)) ^ rk[43];
+        return;
+    }
+#endif
     /* last round: SubBytes + ShiftRows + AddRoundKey, S[x] = byte 2 of Te0[x] */
     out[0] = (((teb<3>(S, s0) << 8) & 0xff000000u) | (teb<2>(S, s1) & 0x00ff0000u) |
               ((teb<1>(S, s2) >> 8) & 0x0000ff00u) | ((teb<0>(S, s3) >> 16) & 0xffu)) ^ rk[40];
