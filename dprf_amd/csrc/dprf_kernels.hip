@@ -522,9 +522,8 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
 /* ================================================================== PDF R2..R4 (MD5 + RC4) */
 /* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
  * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave
- * therefore never conflict, whatever i/j each lane holds.  The kernel's whole LDS footprint is exactly
- * these 16 KiB (charset, PAD and the stop flag are overlaid on the S-box area before the first KSA), so
- * 10 one-wave workgroups fit a CU's 160 KiB. */
+ * therefore never conflict, whatever i/j each lane holds.  16 KiB per wave: 9 such waves fit the ~152 KiB a
+ * CU allocates (tools/lds_occ.hip). */
 #define RC4_WAVE_BYTES 16384
 /* Address of S[j & 0xff] = ((j & 0xfc) << 6) | (j & 3) | lanebase in two half-rate instructions: (j & 3) | lanebase, then byte 1 <- (j & 0xff) >> 2 by an SDWA shift
  * that keeps the other bytes (lanebase < 256); any j (only its low byte counts).  tools/rc4_bench.hip
@@ -567,43 +566,51 @@ DEVI void rc4_identity(uint8_t *S) {
 
 /* KSA with an NK-byte key held LE-packed in k[4].
  *
- * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions 4q..4q+3 are one LDS dword of this lane:
- * group q reads that dword once, and s_r (= S[4q+r] before step r) is its byte r unless an earlier step
- * of the group swapped into that position (S[j] = s with j = 4q+r; a compare-select per earlier step).
- * So the j chain waits on LDS once per four steps.  Every step still reads S[j] and stores both sides of
- * the swap in program order, so LDS is current for every position -- except that the S[i] = S[j] store
- * is issued one step late, after the next step's S[j] read (which missed it when it hit i), and the value
- * it stores -- that read's result, repaired -- is only formed then too: the wave waits for a read one step
- * old instead of the one it has just issued.
- * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs, round 1): the
- * deferred-store schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a register
- * and stored once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain 334 M.  In the
- * product (round 2, tools/ab_libs.sh): repairing the read one step late, 443.7 -> 456 M (R3/R4) and
- * 8.19 -> 8.47 G (R2); byte compares on j itself (v_cmp_eq_u32_sdwa src0_sel:BYTE_0, no j & 0xff) 464 M /
- * 8.70 G.  LLVM still hoists some repairs right after the read they wait on; forcing every wait onto the
- * previous step's read was slower (asm pin 461 M; __builtin_amdgcn_sched_barrier 442 M; a software-pipelined
- * order that waits on the read two steps back 445 M, 452 M without barriers; storing S[i] two steps late
- * 434 M; no deferral at all 405 M): the VALU chain and the LDS issue rate (~10.5 LDS cycles per step, 67 %
- * busy), not the read latency, bound the loop now.  At 16 KiB per wave only 9 waves fit a CU
- * (tools/lds_occ.hip: <= 15,360 B gives 10). */
-template <int NK>
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions Gq..Gq+G-1 (G = 1, 2 or 4 bytes of one LDS
+ * dword of this lane) form group q: the group reads them with one LDS load, and s_r (= S[Gq+r] before step
+ * r) is its byte r unless an earlier step of the group swapped into that position (S[j] = s with j = Gq+r;
+ * a compare-select per earlier step: G(G-1)/2 per group).  So the j chain waits on LDS once per G steps.
+ * Every step still reads S[j] and stores both sides of the swap in program order, so LDS is current for
+ * every position -- except that the S[i] = S[j] store is issued one step late, after the next step's S[j]
+ * read (which missed it when it hit i), and the value it stores -- that read's result, repaired -- is only
+ * formed then too: the wave waits for a read one step old instead of the one it has just issued.
+ * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs, round 1, G = 4):
+ * the deferred-store schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a
+ * register and stored once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain
+ * 334 M.  In the product (round 2, tools/ab_libs.sh): repairing the read one step late, 443.7 -> 456 M
+ * (R3/R4) and 8.19 -> 8.47 G (R2); byte compares on j itself (v_cmp_eq_u32_sdwa src0_sel:BYTE_0, no
+ * j & 0xff) 464 M / 8.70 G; forcing every wait onto the previous step's read was slower (asm pin 461 M;
+ * __builtin_amdgcn_sched_barrier 442 M; software-pipelined 445-452 M; storing S[i] two steps late 434 M; no
+ * deferral 405 M).  Late in round 2, with the key derivation moved to its own wave (k_pdf_r24 below), the
+ * group size was re-measured: G = 4 / 2 / 1 gave R3/R4 481 / 513 / 490 M and R2 9.68 / 9.71 / 9.79 G --
+ * with the MD5s off the RC4 wave the KSA is VALU-issue bound, and G = 2 trades 5 of the 6 in-group
+ * compare-selects of a dword group for one more (exposed) LDS round trip per 4 steps.  At 16 KiB per wave
+ * only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
+#ifndef RC4_GROUP
+#define RC4_GROUP 2                             /* R3/R4 */
+#endif
+#ifndef RC4_GROUP_R2
+#define RC4_GROUP_R2 1
+#endif
+template <int NK, int G = RC4_GROUP>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
+    static_assert(G == 1 || G == 2 || G == 4, "group = one byte, u16 or dword of S");
     rc4_identity(S);
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
     uint32_t j = 0;                             /* only its low byte is meaningful */
-    uint32_t W = 0x03020100u;                   /* dword 0 is the identity */
+    uint32_t W = G == 4 ? 0x03020100u : (G == 2 ? 0x0100u : 0u);   /* group 0 is the identity */
     uint32_t px = 0;                            /* S[i-2] value (repaired), stored at step i-1 */
     uint32_t xr = 0, pm = 0xffffffffu;          /* the previous step's raw S[j] read and its j & 0xff */
 #pragma unroll
-    for (int q = 0; q < 64; q++) {
-        const uint32_t base = 4u * (uint32_t)q;
+    for (int q = 0; q < 256 / G; q++) {
+        const uint32_t base = (uint32_t)(G * q);
         uint32_t s[4], m[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int i = 4 * q + r;
-            uint32_t v = __builtin_amdgcn_ubfe(W, 8 * r, 8);
+        for (int r = 0; r < G; r++) {
+            const int i = G * q + r;
+            uint32_t v = G == 4 ? __builtin_amdgcn_ubfe(W, 8 * r, 8) : G == 1 ? W : (r == 0 ? (W & 0xffu) : (W >> 8));
 #pragma unroll
             for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
             s[r] = v;
@@ -623,7 +630,12 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             xr = x;
             pm = m[r];
         }
-        if (q < 63) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+        if (q < 256 / G - 1) {
+            const int n = G * (q + 1);          /* first position of the next group */
+            if (G == 4) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
+            else if (G == 2) W = *(const uint16_t *)(S + ((n >> 2) << 8) + (n & 3) + lanebase);
+            else W = S[((n >> 2) << 8) + (n & 3) + lanebase];
+        }
     }
     lds_st8(S, (63u << 8) + 3u + lanebase, (pm == 254u) ? px : xr);
 }
@@ -746,108 +758,131 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
     }
 }
 
-/* Candidates per lane: R2's single KSA is short enough that wave launch and the block prologue were a
- * visible part of the kernel, so an R2 lane takes R24_PER_R2 candidates 64 apart; their keys are derived
- * first, while the charset is still in the LDS overlay the KSA then overwrites. */
-#ifndef R24_PER_R2
-#define R24_PER_R2 4
+/* One workgroup = one RC4 wave + one key wave, over NBAT batches of 64 candidates (round 2).
+ *
+ * The RC4 wave owns the workgroup's 16 KiB S-box area (one 256-byte box per lane) and only ever runs KSAs and
+ * PRGAs; the key wave derives the RC4 keys (enumeration + MD5 of the padded password and document tail, and for
+ * R3/R4 the 50 MD5 iterations) of batch b+1 while the RC4 wave runs batch b.  Keys are handed over through the
+ * S-box area while it is free, between two barriers at each batch boundary; charset, PAD and the skip flag sit
+ * in an area of their own (16,720 B per workgroup: still 9 per CU).  The RC4 wave raises its issue priority
+ * (s_setprio 3), so the MD5s take only the VALU cycles the KSA chains leave free.
+ * Why: when one wave did both (round 1 - mid round 2), a wave hashing its keys held its S-box without running
+ * a KSA -- ~8 % of the CU's 9 KSA chains idle for R3/R4, ~15 % for R2.  Measured (tools/ab_libs.sh, MI355X):
+ * R3/R4 fused 464 M, split without / with the priority 458 / 481 M; a key wave that hashes nothing (probe) 484 M,
+ * so the MD5s are fully hidden; then the KSA group size re-tuned (rc4_ksa): R3/R4 513 M, R2 8.77 -> 9.79 G.
+ * Batches per workgroup, R3/R4: 2 / 4 / 8 = 472 / 480 / 481 M (G = 4), 6 / 8 / 12 = 513 / 513 / 507 M (G = 2);
+ * R2: 8 / 16 / 24 = 9.58 / 9.68 / 9.70 G. */
+#ifndef R34_BATCHES
+#define R34_BATCHES 8
 #endif
-template <int R> struct r24_per { static constexpr int v = R == 2 ? R24_PER_R2 : 1; };
-
+#ifndef R2_BATCHES
+#define R2_BATCHES 16
+#endif
+#ifndef R24_PRIO
+#define R24_PRIO 3
+#endif
+template <int R> struct r24_batches { static constexpr uint32_t v = R == 2 ? R2_BATCHES : R34_BATCHES; };
 template <int MODE, int R, int NK>
-__global__ void __launch_bounds__(64, 3)   /* <= 170 VGPRs: 3 waves/SIMD >= the 2.5 the LDS allows */
+__global__ void __launch_bounds__(128, 5)   /* 18 waves per CU (9 workgroups): <= 102 VGPRs */
 k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
-    constexpr int PER = r24_per<R>::v;
+    constexpr uint32_t NBAT = r24_batches<R>::v;
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
-    /* overlaid on the S-box area; all reads of these happen before the first KSA writes it (one wave per
-     * workgroup, LDS operations of a wave complete in order) */
-    uint8_t *cs = S;                                      /* charset, 256 B */
-    uint32_t *flag = (uint32_t *)(S + 256);
-    uint32_t *padw = (uint32_t *)(S + 320);               /* PAD || PAD for the runtime-offset padding */
+    __shared__ __attribute__((aligned(16))) uint32_t aux[64 + 16 + 4];
+    uint8_t *cs = (uint8_t *)aux;                         /* charset, 256 B */
+    uint32_t *padw = aux + 64;                            /* PAD || PAD */
+    uint32_t *flag = aux + 80;
     if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
-    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag, PER)) return;
-    const uint32_t base = blockIdx.x * (64u * PER);
-    const uint32_t lanebase = (threadIdx.x & 63u) << 2;
-    /* range mode: PAD[0:32-pwlen] placed at byte pwlen (pdf...c:136-139), 8 LE words, launch-uniform */
-    uint32_t padtail[8];
+    /* per = candidates per thread of the 128-thread block: 64 * NBAT candidates */
+    if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag, NBAT / 2)) return;
+    const uint32_t base = blockIdx.x * (64u * NBAT);
+    const uint32_t left = e.count - base;                 /* > 0: grid = ceil(count / (64 * NBAT)) */
+    const uint32_t nb = left >= 64u * NBAT ? (uint32_t)NBAT : (left + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t *keyx = (uint32_t *)S;                       /* [4][64] words, only between the two barriers */
+    if (threadIdx.x >= 64u) {
+        /* key wave */
+        uint32_t padtail[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) padtail[j] = 0u;
-    if (MODE == 0) {
-        const uint32_t q = e.pwlen >> 2, r = (e.pwlen & 3u) * 8u;
+        for (int j = 0; j < 8; j++) padtail[j] = 0u;
+        if (MODE == 0) {
+            const uint32_t q = e.pwlen >> 2, r = (e.pwlen & 3u) * 8u;
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const uint32_t lo = r ? (p.pad[t] << r) : p.pad[t];
-            const uint32_t hi = r ? (p.pad[t] >> (32u - r)) : 0u;
+            for (int t = 0; t < 8; t++) {
+                const uint32_t lo = r ? (p.pad[t] << r) : p.pad[t];
+                const uint32_t hi = r ? (p.pad[t] >> (32u - r)) : 0u;
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                if ((uint32_t)j == q + t) padtail[j] |= lo;
-                if ((uint32_t)j == q + t + 1) padtail[j] |= hi;
+                for (int j = 0; j < 8; j++) {
+                    if ((uint32_t)j == q + t) padtail[j] |= lo;
+                    if ((uint32_t)j == q + t + 1) padtail[j] |= hi;
+                }
             }
         }
-    }
-    uint32_t hk[PER][4];
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const uint32_t g0 = base + 64u * k + threadIdx.x;
-        r24_key<MODE, R, NK>(e, p, cs, padw, padtail, g0 < e.count ? g0 : e.count - 1, hk[k]);
-    }
-    /* R3/R4 early reject: every pass first produces only 2 keystream bytes and the candidate survives iff
-     * c19[0:2] equals U[0:2] (byte b of each pass is data[b] ^ keystream[b]).  A wave in which some lane
-     * survives (2^-16 per lane) redoes its candidates with the full keystream and the reference's complete
-     * 16-byte compare (:184-189). */
-    uint8_t *Sw = S;   /* one wave per block: the whole array is this wave's */
+        uint32_t h[4];
+        {
+            const uint32_t g0 = base + lane;
+            r24_key<MODE, R, NK>(e, p, cs, padw, padtail, g0 < e.count ? g0 : e.count - 1, h);
+        }
 #pragma unroll 1
-    for (uint32_t k = 0; k < (uint32_t)PER; k++) {
-        if (base + 64u * k >= e.count) break;                                       /* uniform */
-        const uint32_t g = base + 64u * k + threadIdx.x;
+        for (uint32_t b = 0; b < nb; b++) {
+            __syncthreads();                              /* the RC4 wave is done with batch b-1's S-box */
+#pragma unroll
+            for (int q = 0; q < 4; q++) keyx[64 * q + lane] = h[q];
+            __syncthreads();                              /* batch b's keys are in LDS */
+            if (b + 1u < nb) {
+                const uint32_t g0 = base + 64u * (b + 1u) + lane;
+                r24_key<MODE, R, NK>(e, p, cs, padw, padtail, g0 < e.count ? g0 : e.count - 1, h);
+            }
+        }
+        return;
+    }
+    /* RC4 wave */
+    __builtin_amdgcn_s_setprio(R24_PRIO);
+    uint8_t *Sw = S;
+#pragma unroll 1
+    for (uint32_t b = 0; b < nb; b++) {
+        __syncthreads();
+        __syncthreads();
+        uint32_t h[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) h[q] = keyx[64 * q + lane];
+        const uint32_t g = base + 64u * b + lane;
         const bool valid = g < e.count;
-        const uint32_t h[4] = {hk[0][0], hk[0][1], hk[0][2], hk[0][3]};
-#pragma unroll
-        for (int kk = 0; kk + 1 < PER; kk++)                       /* static rotation, no indexed registers */
-#pragma unroll
-            for (int q = 0; q < 4; q++) hk[kk][q] = hk[kk + 1][q];
         bool ok = false;
         if (R == 2) {
-            /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189) */
+            /* RC4-40 over PAD, compare 32 bytes of U (:161-163, :184-189).  The first 4 keystream bytes decide
+             * for all but 2^-32 of the lanes: a wave continues the same keystream (i = 5.., j carried) only
+             * when one of its lanes matches U[0:4] */
             uint32_t d[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-            rc4_ksa<5>(Sw, lanebase, h);
-#ifndef DPRF_R2_FULL_PRGA
-            /* the first 4 keystream bytes decide for all but a 2^-32 fraction of the lanes: the wave
-             * continues the same keystream (i = 5.., j carried) only when one of its lanes matches U[0:4] */
+            rc4_ksa<5, RC4_GROUP_R2>(Sw, lane << 2, h);
             uint32_t jj = 0;
-            rc4_prga_span<1, 4>(Sw, lanebase, d, jj);
-            ok = false;
+            rc4_prga_span<1, 4>(Sw, lane << 2, d, jj);
             if (__builtin_amdgcn_ballot_w64(valid && d[0] == p.u[0])) {
-                rc4_prga_span<5, 32>(Sw, lanebase, d, jj);
+                rc4_prga_span<5, 32>(Sw, lane << 2, d, jj);
                 ok = true;
 #pragma unroll
                 for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
             }
-#else
-            rc4_prga<32>(Sw, lanebase, d);
-            ok = true;
-#pragma unroll
-            for (int j = 0; j < 8; j++) ok = ok && d[j] == p.u[j];
-#endif
-        } else {
-            /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes */
-            for (uint32_t full = 0; full < 2u; full++) {
-                uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
-                for (uint32_t x = 0; x < 20u; x++) {
-                    const uint32_t xx = x * 0x01010101u;
-                    uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-                    rc4_ksa<NK>(Sw, lanebase, kx);
-                    if (full) rc4_prga<16>(Sw, lanebase, d);
-                    else rc4_prga<2>(Sw, lanebase, d);
-                }
-                if (full) {
-                    ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
-                } else {
-                    const bool pre = ((d[0] ^ p.u[0]) & 0xffffu) == 0u;
-                    if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
-                }
+        } else
+        /* c = RC4(key, MD5(PAD||ID)); c = RC4(key ^ x, c) for x = 1..19 (:167-174), compare 16 bytes.  Early
+         * reject: every pass first produces only 2 keystream bytes and the candidate survives iff c19[0:2]
+         * equals U[0:2]; a wave in which some lane survives (2^-16 per lane) redoes its candidates with the full
+         * keystream and the reference's complete 16-byte compare (:184-189) */
+        for (uint32_t full = 0; full < 2u; full++) {
+            uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
+            for (uint32_t x = 0; x < 20u; x++) {
+                const uint32_t xx = x * 0x01010101u;
+                uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
+                rc4_ksa<NK>(Sw, lane << 2, kx);
+                if (full) rc4_prga<16>(Sw, lane << 2, d);
+                else rc4_prga<2>(Sw, lane << 2, d);
+            }
+            if (full) {
+                ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
+            } else {
+                const bool pre = ((d[0] ^ p.u[0]) & 0xffffu) == 0u;
+                if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
             }
         }
         if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
@@ -883,7 +918,7 @@ hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_resu
 }
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                           uint32_t stop, hipStream_t s) {
-#define L24(M, RR, NK) hipLaunchKernelGGL((k_pdf_r24<M, RR, NK>), GRID(e.count, 64 * r24_per<RR>::v), dim3(64), 0, s, e, p, R, cap, stop)
+#define L24(M, RR, NK) hipLaunchKernelGGL((k_pdf_r24<M, RR, NK>), GRID(e.count, 64 * r24_batches<RR>::v), dim3(128), 0, s, e, p, R, cap, stop)
     if (p.R == 2) { if (e.mode == 0) L24(0, 2, 5); else L24(1, 2, 5); }
     else if (p.n == 16) { if (e.mode == 0) L24(0, 3, 16); else L24(1, 3, 16); }
     else { if (e.mode == 0) L24(0, 3, 5); else L24(1, 3, 5); }

@@ -209,11 +209,13 @@ def test_range_split_consistency(dprf, streams):
     assert s == total and pieces == whole and len(whole) >= 1
 
 
-def test_r2_ragged_ranges(dprf, streams):
-    """R2 lanes take several candidates each (k_pdf_r24, R24_PER_R2): counts that are not a multiple of a
-    block's candidates, and a start that is not block-aligned, give the same hits and counted candidates."""
-    c = ctx_for(dprf, streams, "pdf_synth_r2_key")
-    pw = streams["pdf_synth_r2_key"]["password"]
+@pytest.mark.parametrize("name", ["pdf_synth_r2_key", "pdf_synth_r3_l40_cab"])
+def test_r2_ragged_ranges(dprf, streams, name):
+    """R2-R4 workgroups take several batches of 64 candidates each (k_pdf_r24: R2_BATCHES / R34_BATCHES, a key
+    wave handing keys to an RC4 wave per batch): counts that are not a multiple of a workgroup's candidates, and
+    a start that is not aligned to one, give the same hits and counted candidates."""
+    c = ctx_for(dprf, streams, name)
+    pw = streams[name]["password"]
     idx = 0
     for ch in pw:
         idx = idx * 26 + LOWER.index(ch)

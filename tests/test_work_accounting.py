@@ -60,10 +60,12 @@ def test_pdf_r6_mean_counts(oracle, streams):
 
 
 def test_lds_cycle_model():
-    # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (2 + 4 + 4) + 63 dword reads x 2 + PRGA-2: 5 x 2 + 2 x 4)
-    assert work.LDS_CYCLES["pdf_r34"] * 64 == 20 * (64 * 2 + 256 * 10 + 63 * 2 + 5 * 2 + 2 * 4)
-    # R2: 64 ds_write_b32 x 4 + 256 x (2 reads + 2 stores) - last S[i+1] read + 4 x (3 reads + 2 stores)
-    assert work.LDS_CYCLES["pdf_r2"] * 64 == 64 * 2 + 256 * 10 + 63 * 2 + 4 * (3 * 2 + 2 * 4)
+    # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (2 + 4 + 4) + 127 u16 group reads x 2 + PRGA-2: 5 x 2 + 2 x 4)
+    # + the key hand-off of a batch (4 dword stores x 4 + 4 dword reads x 2)
+    assert work.LDS_CYCLES["pdf_r34"] * 64 == 20 * (64 * 2 + 256 * 10 + 127 * 2 + 5 * 2 + 2 * 4) + 4 * 4 + 4 * 2
+    # R2: 64 addtid x 2 + 256 x (S[j] read + 2 stores) + 255 byte reads of the next S[i] + 4 PRGA bytes x
+    # (3 reads + 2 stores) + the key hand-off
+    assert work.LDS_CYCLES["pdf_r2"] * 64 == 64 * 2 + 256 * 10 + 255 * 2 + 4 * (3 * 2 + 2 * 4) + 4 * 4 + 4 * 2
     assert work.lds_frac("odt", 1e6) is None
     assert abs(work.lds_frac("pdf_r34", 1e6) - 1e6 * work.LDS_CYCLES["pdf_r34"] / (256 * 2.4e9)) < 1e-12
     for fmt in work.LDS_CYCLES:
