@@ -584,15 +584,17 @@ DEVI void rc4_identity(uint8_t *S) {
  * deferral 405 M).  Late in round 2, with the key derivation moved to its own wave (k_pdf_r24 below), the
  * group size was re-measured: G = 4 / 2 / 1 gave R3/R4 481 / 513 / 490 M and R2 9.68 / 9.71 / 9.79 G --
  * with the MD5s off the RC4 wave the KSA is VALU-issue bound, and G = 2 trades 5 of the 6 in-group
- * compare-selects of a dword group for one more (exposed) LDS round trip per 4 steps.  At 16 KiB per wave
- * only 9 waves fit a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
+ * compare-selects of a dword group for one more (exposed) LDS round trip per 4 steps.  DEFER = false stores
+ * S[i] right after its read (no repair): R3/R4 509 vs 512 M, R2 10.08 vs 9.73 G (R2's single KSA per batch
+ * keeps fewer reads in flight), so R2 runs G = 1 without the deferral.  At 16 KiB per wave only 9 waves fit
+ * a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
 #ifndef RC4_GROUP
 #define RC4_GROUP 2                             /* R3/R4 */
 #endif
 #ifndef RC4_GROUP_R2
-#define RC4_GROUP_R2 1
+#define RC4_GROUP_R2 1                          /* R2, and R2 stores S[i] without the deferral */
 #endif
-template <int NK, int G = RC4_GROUP>
+template <int NK, int G = RC4_GROUP, bool DEFER = true>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
     static_assert(G == 1 || G == 2 || G == 4, "group = one byte, u16 or dword of S");
     rc4_identity(S);
@@ -620,6 +622,11 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             m[r] = j & 0xffu;
             const uint32_t a = rc4_addr_sdwa(j, lanebase);
             const uint32_t x = lds_ld8(S, a);
+            if (!DEFER) {
+                lds_st8(S, a, v);
+                lds_st8(S, ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase, x);
+                continue;
+            }
             if (i > 0) {
                 /* the previous step's read missed the store of S[i-2] (issued after it) when it hit i-2 */
                 const uint32_t pv = (pm == (uint32_t)(i - 2)) ? px : xr;
@@ -637,7 +644,7 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
             else W = S[((n >> 2) << 8) + (n & 3) + lanebase];
         }
     }
-    lds_st8(S, (63u << 8) + 3u + lanebase, (pm == 254u) ? px : xr);
+    if (DEFER) lds_st8(S, (63u << 8) + 3u + lanebase, (pm == 254u) ? px : xr);
 }
 
 /* R2 used a one-step-ahead KSA (S[j] and S[i+1] read before the previous step's two stores, both repaired
@@ -855,7 +862,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             uint32_t d[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-            rc4_ksa<5, RC4_GROUP_R2>(Sw, lane << 2, h);
+            rc4_ksa<5, RC4_GROUP_R2, false>(Sw, lane << 2, h);
             uint32_t jj = 0;
             rc4_prga_span<1, 4>(Sw, lane << 2, d, jj);
             if (__builtin_amdgcn_ballot_w64(valid && d[0] == p.u[0])) {
