@@ -312,12 +312,14 @@ def main():
 
     # Rehearsal knobs for the N>1 path on a 1-GPU box (never used by the driver): DPRF_BENCH_SAME_DEVICE=1
     # puts every rank on device 0 and DPRF_BENCH_BACKEND=gloo exchanges through CPU tensors (RCCL refuses two
-    # ranks on one GPU).  The driver's runs use one GPU per rank and RCCL.
+    # ranks on one GPU).  DPRF_BENCH_FORCE_DIST=1 opens the process group even for a single torchrun rank, so
+    # the RCCL init, barrier and MIN/MAX all-reduces run on a 1-GPU box.  The driver's runs use one GPU per
+    # rank and RCCL.
     backend = os.environ.get("DPRF_BENCH_BACKEND", "nccl")
     if os.environ.get("DPRF_BENCH_SAME_DEVICE") == "1":
         local = 0
     dist = None
-    if world > 1:
+    if world > 1 or os.environ.get("DPRF_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
