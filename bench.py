@@ -462,7 +462,7 @@ def main():
                        "charset": "alnum (a-z A-Z 0-9)" if cs == ALNUM else "lowercase", "pwlen": pwlen,
                        "batch_per_gpu": B, "kernel": ctx.kernel,
                        "parallelism": "keyspace shards x%d (%s)" % (
-                           n_gpus, "one process per GPU" if world > 1 else
+                           n_gpus, "one process per GPU" if dist else
                            "one process, %d-device library context" % len(devices))},
             "roofline": roof,
             "cpu_baseline": cpu,

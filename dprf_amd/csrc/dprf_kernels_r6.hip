@@ -43,8 +43,16 @@
 #ifndef R6_TABLES
 #define R6_TABLES 2
 #endif
+#ifndef R6_TE_COPIES
 #define R6_TE_COPIES (32 / R6_TABLES)
+#endif
 #define R6_TE_BYTES (256 * R6_TE_ROW_BYTES)
+/* bytes of a row the tables take; the rest (when at least half a row) holds slot periods */
+#define R6_TE_USED (4 * R6_TABLES * R6_TE_COPIES)
+static_assert(R6_TE_USED <= R6_TE_ROW_BYTES && (R6_TE_COPIES & (R6_TE_COPIES - 1)) == 0, "table rows");
+/* the table whose entry holds S[x] in bytes 3 and 0 (ror16 Te0): the key schedule and the last round
+ * assemble S-box bytes from it and Te0 */
+#define R6_TE2 (R6_TABLES == 4 ? 2 : 1)
 
 DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
     uint32_t t = __umulhi(n, m);
@@ -89,9 +97,9 @@ DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[4
 #pragma unroll
     for (int i = 0; i < 10; i++) {
         const uint32_t t = rk[4 * i + 3];
-#if R6_TABLES == 2
+#if R6_TABLES >= 2
         /* SubWord(RotWord(t)): S[x] in bytes 3, 0 of Te2[x] and 2, 1 of Te0[x] (see the last round) */
-        const uint32_t sw = perm(tebt<1, 2>(S, t), teb<1>(S, t), 0x07020c0cu) | perm(teb<0>(S, t), tebt<1, 3>(S, t), 0x0c0c0500u);
+        const uint32_t sw = perm(tebt<R6_TE2, 2>(S, t), teb<1>(S, t), 0x07020c0cu) | perm(teb<0>(S, t), tebt<R6_TE2, 3>(S, t), 0x0c0c0500u);
 #else
         /* SubWord(RotWord(t)) with S[x] = byte 2 of Te0[x] */
         const uint32_t sw = ((teb<2>(S, t) << 8) & 0xff000000u) | (teb<1>(S, t) & 0x00ff0000u) |
@@ -137,15 +145,15 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
 #endif
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-#if R6_TABLES == 2
+#if R6_TABLES >= 2
     /* last round: SubBytes + ShiftRows + AddRoundKey.  S[x] sits in bytes 2 and 1 of Te0[x] and in bytes 3
      * and 0 of Te2[x], i.e. already where each output byte needs it: two v_perm and one or-xor per word */
     {
         const uint32_t HI = 0x07020c0cu, LO = 0x0c0c0500u;   /* src0.b3 src1.b2 0 0 | 0 0 src0.b1 src1.b0 */
-        out[0] = (perm(tebt<1, 3>(S, s0), teb<2>(S, s1), HI) | perm(teb<1>(S, s2), tebt<1, 0>(S, s3), LO)) ^ rk[40];
-        out[1] = (perm(tebt<1, 3>(S, s1), teb<2>(S, s2), HI) | perm(teb<1>(S, s3), tebt<1, 0>(S, s0), LO)) ^ rk[41];
-        out[2] = (perm(tebt<1, 3>(S, s2), teb<2>(S, s3), HI) | perm(teb<1>(S, s0), tebt<1, 0>(S, s1), LO)) ^ rk[42];
-        out[3] = (perm(tebt<1, 3>(S, s3), teb<2>(S, s0), HI) | perm(teb<1>(S, s1), tebt<1, 0>(S, s2), LO)) ^ rk[43];
+        out[0] = (perm(tebt<R6_TE2, 3>(S, s0), teb<2>(S, s1), HI) | perm(teb<1>(S, s2), tebt<R6_TE2, 0>(S, s3), LO)) ^ rk[40];
+        out[1] = (perm(tebt<R6_TE2, 3>(S, s1), teb<2>(S, s2), HI) | perm(teb<1>(S, s3), tebt<R6_TE2, 0>(S, s0), LO)) ^ rk[41];
+        out[2] = (perm(tebt<R6_TE2, 3>(S, s2), teb<2>(S, s3), HI) | perm(teb<1>(S, s0), tebt<R6_TE2, 0>(S, s1), LO)) ^ rk[42];
+        out[3] = (perm(tebt<R6_TE2, 3>(S, s3), teb<2>(S, s0), HI) | perm(teb<1>(S, s1), tebt<R6_TE2, 0>(S, s2), LO)) ^ rk[43];
         return;
     }
 #endif
@@ -433,7 +441,7 @@ struct r6_shared {
 
 DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, uint32_t slot, uint32_t lane) {
     r6_lds S;
-    if (slot < te_slots) {
+    if (slot < te_slots) {                  /* only when the tables leave the upper half of each row */
         S.pat = lds_addr(r6_te) + (slot >> 5) * pat_words * 256u;
         S.lanebase = 128u + ((slot & 31u) << 2);
     } else {
@@ -549,9 +557,10 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nthr = blockDim.x;
     /* Te0 copies into bytes 0..127 of each row; the upper halves are slot periods */
     /* the tables' copies fill bytes 0..127 of each row: table t = ror(Te0, 8t) (16t with two tables) */
-    for (uint32_t k = tid; k < 256u * 32u; k += nthr) {
-        const uint32_t t = (k & 31u) / R6_TE_COPIES;
-        r6_te[(k >> 5) * (R6_TE_ROW_BYTES / 4) + (k & 31u)] = ror32(T->te0[k >> 5], (R6_TABLES == 2 ? 16 : 8) * t);
+    constexpr uint32_t TW = R6_TE_USED / 4;                                     /* table words per row */
+    for (uint32_t k = tid; k < 256u * TW; k += nthr) {
+        const uint32_t x = k / TW, c = k % TW, t = c / R6_TE_COPIES;
+        r6_te[x * (R6_TE_ROW_BYTES / 4) + c] = ror32(T->te0[x], (R6_TABLES == 2 ? 16 : 8) * t);
     }
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
@@ -636,7 +645,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
  * in the dynamic LDS left next to the table and the shared block (160 KiB per workgroup). */
 static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots, size_t *shm) {
     const size_t fixed = R6_TE_BYTES + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
-    const uint32_t te_groups = 256u / pat_words;
+    const uint32_t te_groups = R6_TE_USED <= 128 ? 256u / pat_words : 0u;
     uint32_t te = te_groups * 32u;
     uint32_t dyn = (uint32_t)((160u * 1024u - fixed) / ((size_t)pat_words * 256u)) * 64u;
     if (te > R6_MAX_SLOTS) te = R6_MAX_SLOTS;
@@ -655,8 +664,9 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     /* longest password of the launch (list mode: the host's maximum over the chunk): the period length
      * and with it the slots per CU follow the actual candidates, not the 64-byte slot width */
     const uint32_t lmax = e.pwlen < 4u * DPRF_SLOT_WORDS ? e.pwlen : 4u * DPRF_SLOT_WORDS;
-    /* period (lmax + 64) + 16 wrap bytes, + 4 words read past the last block start */
-    const uint32_t pat_words = (lmax + 64u + 16u + 3u) / 4u + 1u;
+    /* period (lmax + 64) + 16 wrap bytes: a block read starts at byte o < lmax + 64 and takes the 5 words
+     * from word o / 4 (the wrap bytes end inside them) */
+    const uint32_t pat_words = ((lmax + 63u) >> 2) + 5u;
     uint32_t nslots = 0, te_slots = 0;
     size_t shm = 0;
     r6_capacity(pat_words, &nslots, &te_slots, &shm);
