@@ -566,90 +566,64 @@ DEVI void rc4_identity(uint8_t *S) {
 
 /* KSA with an NK-byte key held LE-packed in k[4].
  *
- * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions Gq..Gq+G-1 (G = 1, 2 or 4 bytes of one LDS
- * dword of this lane) form group q: the group reads them with one LDS load, and s_r (= S[Gq+r] before step
- * r) is its byte r unless an earlier step of the group swapped into that position (S[j] = s with j = Gq+r;
- * a compare-select per earlier step: G(G-1)/2 per group).  So the j chain waits on LDS once per G steps.
- * Every step still reads S[j] and stores both sides of the swap in program order, so LDS is current for
- * every position -- except that the S[i] = S[j] store is issued one step late, after the next step's S[j]
- * read (which missed it when it hit i), and the value it stores -- that read's result, repaired -- is only
- * formed then too: the wave waits for a read one step old instead of the one it has just issued.
- * Measured on 4 Mi lanes of 20 x (KSA + PRGA16) (tools/rc4_bench.hip, bit-identical outputs, round 1, G = 4):
- * the deferred-store schedule 431 M cand/s; without the deferred store 409 M; the S[i] side kept in a
- * register and stored once per dword (two v_perm per step) 390 M; one-step-ahead prefetch 370 M; plain
- * 334 M.  In the product (round 2, tools/ab_libs.sh): repairing the read one step late, 443.7 -> 456 M
- * (R3/R4) and 8.19 -> 8.47 G (R2); byte compares on j itself (v_cmp_eq_u32_sdwa src0_sel:BYTE_0, no
- * j & 0xff) 464 M / 8.70 G; forcing every wait onto the previous step's read was slower (asm pin 461 M;
- * __builtin_amdgcn_sched_barrier 442 M; software-pipelined 445-452 M; storing S[i] two steps late 434 M; no
- * deferral 405 M).  Late in round 2, with the key derivation moved to its own wave (k_pdf_r24 below), the
- * group size was re-measured: G = 4 / 2 / 1 gave R3/R4 481 / 513 / 490 M and R2 9.68 / 9.71 / 9.79 G --
- * with the MD5s off the RC4 wave the KSA is VALU-issue bound, and G = 2 trades 5 of the 6 in-group
- * compare-selects of a dword group for one more (exposed) LDS round trip per 4 steps.  DEFER = false stores
- * S[i] right after its read (no repair): R3/R4 509 vs 512 M, R2 10.08 vs 9.73 G (R2's single KSA per batch
- * keeps fewer reads in flight), so R2 runs G = 1 without the deferral.  At 16 KiB per wave only 9 waves fit
- * a CU (tools/lds_occ.hip: <= 15,360 B gives 10). */
-#ifndef RC4_GROUP
-#define RC4_GROUP 2                             /* R3/R4 */
-#endif
-#ifndef RC4_GROUP_R2
-#define RC4_GROUP_R2 1                          /* R2, and R2 stores S[i] without the deferral */
-#endif
-template <int NK, int G = RC4_GROUP, bool DEFER = true>
+ * Step i: j += S[i] + K[i % NK]; swap(S[i], S[j]).  Positions i0 = 2q, i1 = 2q + 1 (one u16 of this lane's
+ * S-box) form group q, read with one LDS load W that was issued at the end of group q-1:
+ *  - step 0: v0 = S[i0] = byte 0 of W; j += v0 + key byte; x0 = S[j] is read and S[j] = v0 stored at once;
+ *  - step 1: v1 = byte 1 of W, or v0 if step 0 swapped into i1; x1 = S[j] read, S[j] = v1 stored;
+ *  - the S[i] sides are NOT stored yet: the next group's W is read first (after both S[j] stores, the only
+ *    stores that can touch its positions), and only then S[i0] = (v1 if step 1 hit i0, else x0) and
+ *    S[i1] = x1 (x0 instead when step 1 read i0, whose store was still pending) -- one u16 store, LLVM merges
+ *    the two.  The next group's first S[j] read comes after that store, so it needs no repair.
+ * The wave waits on LDS once per group: for x1, with W right behind it.
+ *
+ * History (tools/rc4_bench.hip, tools/ab_libs.sh): until late round 2 each S[i] store was
+ * deferred by one step only (stored at the next step, the read repaired when it hit i) and W was read after
+ * the group's stores, so a group waited twice -- for W, then for x0 at the next step's deferred store, a
+ * few instructions after its read: R3/R4 513 M, R2 10.2 G cand/s.  Group-deferred with the W read pinned
+ * ahead of the stores: 561 M / 11.3 G.  Without the pin LLVM sinks the W read below the stores (it can
+ * prove they do not alias), and the second wait is back: 494 M.  The same with dword groups (G = 4: 12
+ * compare-selects per 4 steps) 424 M / 8.6 G: VALU-bound. */
+template <int NK>
 DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
-    static_assert(G == 1 || G == 2 || G == 4, "group = one byte, u16 or dword of S");
     rc4_identity(S);
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = (k[q >> 2] >> (8 * (q & 3))) & 0xffu;
     uint32_t j = 0;                             /* only its low byte is meaningful */
-    uint32_t W = G == 4 ? 0x03020100u : (G == 2 ? 0x0100u : 0u);   /* group 0 is the identity */
-    uint32_t px = 0;                            /* S[i-2] value (repaired), stored at step i-1 */
-    uint32_t xr = 0, pm = 0xffffffffu;          /* the previous step's raw S[j] read and its j & 0xff */
+    uint32_t W = 0x0100u;                       /* group 0 is the identity */
 #pragma unroll
-    for (int q = 0; q < 256 / G; q++) {
-        const uint32_t base = (uint32_t)(G * q);
-        uint32_t s[4], m[4];
-#pragma unroll
-        for (int r = 0; r < G; r++) {
-            const int i = G * q + r;
-            uint32_t v = G == 4 ? __builtin_amdgcn_ubfe(W, 8 * r, 8) : G == 1 ? W : (r == 0 ? (W & 0xffu) : (W >> 8));
-#pragma unroll
-            for (int rr = 0; rr < r; rr++) v = (m[rr] == base + (uint32_t)r) ? s[rr] : v;
-            s[r] = v;
-            j = j + v + kb[i % NK];
-            /* used only in compares, which LLVM folds into SDWA byte selects of j (the address asm takes
-             * byte 0 of j itself, so nothing needs the masked value) */
-            m[r] = j & 0xffu;
-            const uint32_t a = rc4_addr_sdwa(j, lanebase);
-            const uint32_t x = lds_ld8(S, a);
-            if (!DEFER) {
-                lds_st8(S, a, v);
-                lds_st8(S, ((uint32_t)(i >> 2) << 8) + (uint32_t)(i & 3) + lanebase, x);
-                continue;
-            }
-            if (i > 0) {
-                /* the previous step's read missed the store of S[i-2] (issued after it) when it hit i-2 */
-                const uint32_t pv = (pm == (uint32_t)(i - 2)) ? px : xr;
-                lds_st8(S, ((uint32_t)((i - 1) >> 2) << 8) + (uint32_t)((i - 1) & 3) + lanebase, pv);
-                px = pv;
-            }
-            lds_st8(S, a, v);
-            xr = x;
-            pm = m[r];
+    for (int q = 0; q < 128; q++) {
+        const uint32_t i0 = 2u * q, i1 = i0 + 1u;
+        const uint32_t p0 = ((i0 >> 2) << 8) + (i0 & 3u) + lanebase;
+        const uint32_t v0 = W & 0xffu;
+        j = j + v0 + kb[i0 % NK];
+        const uint32_t a0 = rc4_addr_sdwa(j, lanebase);
+        /* m0, m1 are used only in compares, which LLVM folds into SDWA byte selects of j */
+        const uint32_t m0 = j & 0xffu;
+        const uint32_t x0 = lds_ld8(S, a0);
+        lds_st8(S, a0, v0);
+        const uint32_t v1 = (m0 == i1) ? v0 : (W >> 8);
+        j = j + v1 + kb[i1 % NK];
+        const uint32_t a1 = rc4_addr_sdwa(j, lanebase);
+        const uint32_t m1 = j & 0xffu;
+        uint32_t x1 = lds_ld8(S, a1);
+        lds_st8(S, a1, v1);
+        if (q < 127) {
+            const uint32_t n = i0 + 2u;
+            W = *(const uint16_t *)(S + ((n >> 2) << 8) + (n & 3u) + lanebase);
+            /* keep the read ahead of the deferred stores (they wait for x1; W must already be in flight) */
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (q < 256 / G - 1) {
-            const int n = G * (q + 1);          /* first position of the next group */
-            if (G == 4) W = *(const uint32_t *)(S + ((q + 1) << 8) + lanebase);
-            else if (G == 2) W = *(const uint16_t *)(S + ((n >> 2) << 8) + (n & 3) + lanebase);
-            else W = S[((n >> 2) << 8) + (n & 3) + lanebase];
-        }
+        const bool hit = m1 == i0;
+        x1 = hit ? x0 : x1;
+        lds_st8(S, p0, hit ? v1 : x0);
+        lds_st8(S, p0 + 1u, x1);
     }
-    if (DEFER) lds_st8(S, (63u << 8) + 3u + lanebase, (pm == 254u) ? px : xr);
 }
 
-/* R2 used a one-step-ahead KSA (S[j] and S[i+1] read before the previous step's two stores, both repaired
- * in registers) until round 2: re-measured after the SDWA address and the 4-byte PRGA reject, the grouped
- * deferred-store rc4_ksa above is 23 % faster for R2 too (6.67 -> 8.20 G cand/s, tools/ab_libs.sh). */
+/* R2 (one KSA per candidate) runs the same rc4_ksa; its round-1 one-step-ahead KSA (S[j] and S[i+1] read
+ * before the previous step's two stores, both repaired in registers) was 23 % slower once measured against
+ * the grouped schedule (6.67 -> 8.20 G cand/s, round 2). */
 /* PRGA bytes FROM..TO (1-based keystream positions), j carried in and out, XORed into d[] (LE-packed) */
 template <int FROM, int TO>
 DEVI void rc4_prga_span(uint8_t *S, uint32_t lanebase, uint32_t d[], uint32_t &j) {
@@ -862,7 +836,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             uint32_t d[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-            rc4_ksa<5, RC4_GROUP_R2, false>(Sw, lane << 2, h);
+            rc4_ksa<5>(Sw, lane << 2, h);
             uint32_t jj = 0;
             rc4_prga_span<1, 4>(Sw, lane << 2, d, jj);
             if (__builtin_amdgcn_ballot_w64(valid && d[0] == p.u[0])) {
