@@ -752,12 +752,14 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
  * R3/R4 fused 464 M, split without / with the priority 458 / 481 M; a key wave that hashes nothing (probe) 484 M,
  * so the MD5s are fully hidden; then the KSA group size re-tuned (rc4_ksa): R3/R4 513 M, R2 8.77 -> 9.79 G.
  * Batches per workgroup, R3/R4: 2 / 4 / 8 = 472 / 480 / 481 M (G = 4), 6 / 8 / 12 = 513 / 513 / 507 M (G = 2);
- * R2: 8 / 16 / 24 = 9.58 / 9.68 / 9.70 G. */
+ * R2: 8 / 16 / 24 = 9.58 / 9.68 / 9.70 G.  Re-measured on the group-deferred KSA: R3/R4 6 / 8 / 12 batches
+ * 559 / 560 / 557 M, priority 0 / 1 / 3 529 / 560 / 560 M; R2 8 / 16 / 24 batches 11.08 / 11.25 / 11.32 G,
+ * priority 0 10.56 G. */
 #ifndef R34_BATCHES
 #define R34_BATCHES 8
 #endif
 #ifndef R2_BATCHES
-#define R2_BATCHES 16
+#define R2_BATCHES 24
 #endif
 #ifndef R24_PRIO
 #define R24_PRIO 3
