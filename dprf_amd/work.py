@@ -136,12 +136,12 @@ BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "lds", "pd
 #   R3/R4 (rc4_ksa, k_pdf_r24; groups of two positions with group-deferred S[i] stores, late round 2):
 #   identity 64 x addtid (128) + 256 steps x (S[j] read 2 + S[j] store 4) + 128 u16 stores of the two S[i]
 #   sides (512) + 127 u16 reads of the next group (254) = 2,430 per KSA; the 2-byte PRGA of the early-reject
-#   pass 5 reads + 2 stores = 18; 20 passes; + the key hand-off per batch of 64 (key wave: 4 dword stores,
+#   pass, swaps kept in registers: one dword + 4 byte reads, no stores = 10; 20 passes; + the key hand-off per batch of 64 (key wave: 4 dword stores,
 #   RC4 wave: 4 dword reads = 24 cycles).
 #   R2 (the same rc4_ksa): identity 128 + 256 x 6 + 512 + 254 + 4 PRGA bytes x (3 reads + 2 stores = 14)
 #   (the other 28 bytes only in the 2^-32 of waves where a lane matches U[0:4]) + the key hand-off 24.
 LDS_CYCLES = {
-    "pdf_r34": (20 * (128 + 256 * 6 + 128 * 4 + 127 * 2 + 18) + 24) / 64.0,
+    "pdf_r34": (20 * (128 + 256 * 6 + 128 * 4 + 127 * 2 + 10) + 24) / 64.0,
     "pdf_r2": (128 + 256 * 6 + 128 * 4 + 127 * 2 + 4 * 14 + 24) / 64.0,
 }
 PEAK_LDS_CYCLES_PER_S = 256 * 2.4e9          # one LDS per CU

@@ -61,9 +61,9 @@ def test_pdf_r6_mean_counts(oracle, streams):
 
 def test_lds_cycle_model():
     # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (S[j] read 2 + S[j] store 4) + 128 u16 stores of the
-    # group-deferred S[i] sides x 4 + 127 u16 group reads x 2 + PRGA-2: 5 x 2 + 2 x 4) + the key hand-off of
-    # a batch (4 dword stores x 4 + 4 dword reads x 2)
-    assert work.LDS_CYCLES["pdf_r34"] * 64 == (20 * (64 * 2 + 256 * 6 + 128 * 4 + 127 * 2 + 5 * 2 + 2 * 4)
+    # group-deferred S[i] sides x 4 + 127 u16 group reads x 2 + PRGA-2 in registers: 5 reads x 2) + the key
+    # hand-off of a batch (4 dword stores x 4 + 4 dword reads x 2)
+    assert work.LDS_CYCLES["pdf_r34"] * 64 == (20 * (64 * 2 + 256 * 6 + 128 * 4 + 127 * 2 + 5 * 2)
                                               + 4 * 4 + 4 * 2)
     # R2: the same KSA + 4 PRGA bytes x (3 reads + 2 stores) + the key hand-off
     assert work.LDS_CYCLES["pdf_r2"] * 64 == (64 * 2 + 256 * 6 + 128 * 4 + 127 * 2 + 4 * (3 * 2 + 2 * 4)
@@ -76,15 +76,16 @@ def test_lds_cycle_model():
 
 def test_lds_instruction_count_matches_rocprof():
     """The KSA's LDS instruction count behind LDS_CYCLES against rocprof's SQ_INSTS_LDS of the kernel
-    (profiles/prof_pdf_r*_r02i.json, MI355X): per workgroup (one RC4 wave + one key wave) over its batches."""
+    (profiles/prof_pdf_r*_r02j.json, MI355X): per workgroup (one RC4 wave + one key wave) over its batches."""
     import json
     import os
     ksa = 64 + 256 + 256 + 128 + 127              # addtid, S[j] reads, S[j] stores, S[i] u16 stores, u16 reads
-    per_batch = {"pdf_r34": 20 * (ksa + 5 + 2) + 4 + 4, "pdf_r2": ksa + 4 * 5 + 4 + 4}
-    batches = {"pdf_r34": 8, "pdf_r2": 16}
+    # + PRGA (R3/R4: 5 reads; R2: 4 bytes x (3 reads + 2 stores)) + the key hand-off (4 reads + 4 stores)
+    per_batch = {"pdf_r34": 20 * (ksa + 5) + 4 + 4, "pdf_r2": ksa + 4 * 5 + 4 + 4}
+    batches = {"pdf_r34": 8, "pdf_r2": 24}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for fmt in per_batch:
-        d = json.load(open(os.path.join(root, "profiles", "prof_%s_r02i.json" % fmt)))
+        d = json.load(open(os.path.join(root, "profiles", "prof_%s_r02j.json" % fmt)))
         (pd,) = [v["per_dispatch"] for k, v in d["counters"].items() if "k_pdf_r24" in k]
         measured = pd["SQ_INSTS_LDS"] / pd["SQ_WAVES"] * 2
         model = per_batch[fmt] * batches[fmt]
