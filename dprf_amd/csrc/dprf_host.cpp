@@ -194,6 +194,7 @@ struct dprf_ctx {
     uint8_t *h_slots = nullptr;       /* list-mode staging (pinned, portable), shared by the lanes */
     uint8_t *h_lens = nullptr;
     size_t h_cap = 0;
+    std::mutex call_mu;               /* one call at a time per context: the lanes' buffers are per call */
 };
 
 static const char *kind_name(kernel_kind k) {
@@ -696,6 +697,7 @@ extern "C" int dprf_search_range(dprf_ctx *c, const uint8_t *charset, int cslen,
     if ((long double)start + (long double)count > space)
         return fail(DPRF_E_INVALID, "range [%llu, +%llu) exceeds the keyspace %d^%d", (unsigned long long)start,
                     (unsigned long long)count, cslen, pwlen);
+    std::lock_guard<std::mutex> call_lock(c->call_mu);
     const auto t0 = std::chrono::steady_clock::now();
     if (c->kind == K_NONE || count == 0) { empty_result(count, nhits, stats, c->lanes.size()); return DPRF_OK; }
     uint32_t m, s;
@@ -802,6 +804,7 @@ extern "C" int dprf_list_status(const dprf_ctx *c, const uint8_t *blob, const ui
 extern "C" int dprf_verify_list(dprf_ctx *c, const uint8_t *blob, const uint64_t *offsets, int64_t n,
                                 int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats) {
     if (!c || (n > 0 && (!blob || !offsets)) || n < 0) return fail(DPRF_E_INVALID, "dprf_verify_list: bad argument");
+    std::lock_guard<std::mutex> call_lock(c->call_mu);
     const auto t0 = std::chrono::steady_clock::now();
     const size_t SB = DPRF_SLOT_WORDS * 4;
     if ((size_t)n > c->h_cap) {

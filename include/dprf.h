@@ -16,8 +16,8 @@
  * thread and one HIP stream per device for the duration of a call: dprf_search_range / dprf_verify_list
  * fan the call out over the devices inside the library (the reference's 4 worker processes on one queue,
  * brute_force.py:70-73 / :92-95, become one worker thread per GPU on one shared chunk cursor).  Calls on
- * DIFFERENT contexts may run concurrently from different threads; calls on the SAME context must be
- * serialised by the caller.
+ * DIFFERENT contexts may run concurrently from different threads; calls on the SAME context are
+ * serialised by the library (a second caller waits for the first call to return).
  * Ownership: the caller owns every buffer it passes; they are read/written only during the call.
  */
 #ifndef DPRF_H

@@ -298,6 +298,29 @@ def test_multi_device_context_equals_one_device(dprf, streams):
     assert res[(0,)] == res[(0, 0)]
 
 
+def test_concurrent_calls_on_one_context_are_serialised(dprf, streams):
+    """Calls on the same context from several threads (ctypes drops the GIL) are serialised by the library:
+    each thread gets exactly the single-threaded hit set and candidate count."""
+    import threading
+    from dprf_amd import brute_force as bf
+    fields = bf.parse_verification_data(streams["odt_testdoc_e"]["stream"])
+    start, count = 62 ** 5 // 2, 1 << 22
+    with dprf.Context(fields, devices=[0, 0]) as c:
+        want, nwant, _ = c.search_range(ALNUM, 5, start, count, cap=1 << 12)
+        out = [None] * 4
+
+        def run(k):
+            out[k] = c.search_range(ALNUM, 5, start, count, cap=1 << 12)
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for hits, n, st in out:
+            assert hits == want and n == nwant and st["candidates"] == count
+
+
 def test_stop_on_first_lowest_across_blocks_and_launches(dprf, streams):
     """The right password planted at several list positions spread over blocks and launches (Office: 2^19
     candidates per launch): stop_on_first answers the lowest position, on one and on two devices, whatever
