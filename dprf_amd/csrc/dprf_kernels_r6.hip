@@ -14,7 +14,7 @@
  *    its own LDS bank column ([word][lane], so a lane's words share one bank) and pulls each 16-byte
  *    block out of it with 5 ds_read_b32 + 4 v_perm; ciphertext goes straight into the SHA message
  *    registers 64 bytes (4 AES blocks) at a time.
- *  - AES T-tables: Te0 and Te2 = ror16(Te0), each replicated 16x across banks (lane l reads copy l%16);
+ *  - AES T-tables: Te0 and Te2 = ror16(Te0), each replicated 32x across banks (lane l reads copy l%32);
  *    a round column is Te0[a] ^ Te2[c] ^ ror8(Te0[b] ^ Te2[d] ^ rol8 k), one rotate instead of three.
  *    The last round takes S[x] from byte 2 of Te0[x].
  *  - Persistent lanes: a wave owns a contiguous range of candidates; a lane that finishes its
@@ -29,22 +29,25 @@
 
 #include <mutex>
 
-/* T-tables in bytes 0..127 of 256-byte rows, row x = entry x: R6_TABLES tables (table t = ror(Te0, 8t), or
- * Te2 = ror16(Te0) as the second of two), each replicated 32/R6_TABLES times; copy c of table t at byte
- * 256*x + 4*(c + t*copies), lane l reads copy l%copies.  The address of byte k of a state word is ONE
- * v_perm: byte 1 <- byte k of the word, byte 0 <- 4*(lane%copies), bytes 2-3 <- 0 (+ the table's offset
- * as an immediate).  Bytes 128..255 of every row are free: they hold the periods of 32-slot groups
- * (slot_lds), so the 64 KiB the addressing needs is not lost.
- * Two tables (default): a 32-lane group of a ds_read_b32 ({0-31}, {32-63}: MI355X_MICROARCH.md LDS table)
- * meets each of 16 banks twice (2-way conflicts) but a column needs one rotate instead of three --
- * 3.02 -> 3.18 M cand/s over one table × 32 copies (conflict-free); four tables × 8 copies (no rotates,
- * 4-way conflicts): 1.91 M.  (round 2, tools/ab_libs.sh pdf_r6) */
+/* T-tables in 256-byte rows, row x = entry x: R6_TABLES tables (table t = ror(Te0, 8t), or Te2 = ror16(Te0)
+ * as the second of two), each replicated R6_TE_COPIES times; copy c of table t at byte 256*x +
+ * 4*(c + t*copies), lane l reads copy l%copies.  The address of byte k of a state word is ONE v_perm: byte 1
+ * <- byte k of the word, byte 0 <- 4*(lane%copies), bytes 2-3 <- 0 (+ the table's offset as an immediate).
+ * Default: Te0 and Te2, 32 copies each, filling the rows: the 32 lanes of a ds_read_b32 half ({0-31},
+ * {32-63}: MI355X_MICROARCH.md LDS table) meet 32 different banks, and a column needs one rotate instead of
+ * three.  Measured (round 2, tools/ab_libs.sh pdf_r6): one table × 32 copies (conflict-free, slot periods in
+ * the free row halves, 1,248 slots) 3.02 M cand/s; Te0 + Te2 × 16 copies in the row halves (2-way
+ * conflicts, 1,248 slots) 3.18 M; Te0 + Te2 × 32 copies (no conflicts, 960 slots, all in the dynamic area)
+ * 3.50 M; four tables × 16 copies (no rotates, 2-way conflicts, 960 slots) 3.06 M; four × 8 (4-way) 1.91 M.
+ * Bank conflicts cost more than rotates or slots: they lengthen every round's dependent lookups.  With
+ * R6_TE_USED <= 128 (fewer copies) bytes 128..255 of each row hold the periods of 32-slot groups
+ * (slot_lds). */
 #define R6_TE_ROW_BYTES 256
 #ifndef R6_TABLES
 #define R6_TABLES 2
 #endif
 #ifndef R6_TE_COPIES
-#define R6_TE_COPIES (32 / R6_TABLES)
+#define R6_TE_COPIES (R6_TABLES == 4 ? 8 : 32)   /* 2 x 32: whole 256-byte rows, no bank conflicts */
 #endif
 #define R6_TE_BYTES (256 * R6_TE_ROW_BYTES)
 /* bytes of a row the tables take; the rest (when at least half a row) holds slot periods */
@@ -411,9 +414,10 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
  * (slots holding a candidate) only falls when a slot finds the launch's cursor exhausted; at 0 every wave
  * leaves the loop, and the grid drains.
  *
- * Pattern areas: slots [0, te_slots) live in the free upper halves of the Te0 rows in groups of 32
- * (column 128 + 4*(slot%32)), the rest in the dynamic area in groups of 64 (column 4*(slot%64)); rows are
- * 256 bytes apart in both, so r6_read16 and friends see one layout. */
+ * Pattern areas: the dynamic area holds slots in groups of 64 (column 4*(slot%64)); when the tables take only
+ * half of each row (R6_TE_USED <= 128, not the default) slots [0, te_slots) live in the free upper halves in
+ * groups of 32 (column 128 + 4*(slot%32)).  Rows are 256 bytes apart in both, so r6_read16 and friends see
+ * one layout. */
 #ifndef R6_LANES
 #define R6_LANES 768
 #endif
@@ -555,8 +559,8 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
     const uint32_t patbase = lds_addr(smem) + 256u + (uint32_t)((sizeof(r6_shared) + 15) / 16 * 16);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nthr = blockDim.x;
-    /* Te0 copies into bytes 0..127 of each row; the upper halves are slot periods */
-    /* the tables' copies fill bytes 0..127 of each row: table t = ror(Te0, 8t) (16t with two tables) */
+    /* the tables' copies fill the first R6_TE_USED bytes of each row: table t = ror(Te0, 8t) (16t with two
+     * tables); the rest of a row, if any, holds slot periods */
     constexpr uint32_t TW = R6_TE_USED / 4;                                     /* table words per row */
     for (uint32_t k = tid; k < 256u * TW; k += nthr) {
         const uint32_t x = k / TW, c = k % TW, t = c / R6_TE_COPIES;
