@@ -148,6 +148,14 @@ DEVI void sha256_msg2(uint32_t m[32], uint32_t total, uint32_t out[8]) {
     if (two) sha256_compress(out, b1);
 }
 
+/* The file is compiled twice (Makefile): the Office kernels alone (DPRF_PART_OFFICE) and everything else
+ * (DPRF_PART_MAIN), each with the LLVM machine-scheduler strategy that measured fastest for it. */
+#if !defined(DPRF_PART_OFFICE) && !defined(DPRF_PART_MAIN)
+#define DPRF_PART_OFFICE
+#define DPRF_PART_MAIN
+#endif
+
+#ifdef DPRF_PART_OFFICE
 /* ================================================================== Office (ECMA-376 Standard) */
 /* Two launches per batch.  k_office_kdf runs the 50,002 dependent SHA-1s at 8 waves/SIMD (<= 64 VGPRs)
  * and leaves the AES-128 key X1[0:16] of every candidate in HBM ([word][candidate], coalesced);
@@ -239,6 +247,9 @@ k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf
     if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
 }
 
+#endif /* DPRF_PART_OFFICE */
+
+#ifdef DPRF_PART_MAIN
 /* ================================================================== ODF 1.2 (AES-256-CBC, PBKDF2-HMAC-SHA1) */
 /* Two launches per batch, as for Office: k_odt_kdf (SHA-256 start key + PBKDF2, 8 waves/SIMD) leaves the
  * 32-byte AES-256 key of every candidate in HBM; k_odt_check decrypts and verifies. */
@@ -876,9 +887,12 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     }
 }
 
+#endif /* DPRF_PART_MAIN */
+
 /* ------------------------------------------------------------------ launchers */
 #define GRID(n, b) dim3(((n) + (b) - 1) / (b))
 
+#ifdef DPRF_PART_OFFICE
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
@@ -888,6 +902,9 @@ hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const 
     hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
+#endif
+
+#ifdef DPRF_PART_MAIN
 hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_aes_tables *T,
                       dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
@@ -912,3 +929,4 @@ hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_res
 #undef L24
     return hipGetLastError();
 }
+#endif /* DPRF_PART_MAIN */

@@ -1,14 +1,12 @@
 #!/bin/bash
 # Build an A/B variant of libdprf.so with extra compiler flags: tools/build_variant.sh <name> <flags...>
-# -> build/ab/libdprf_<name>.so (run on the CPU side; the .so travels to the GPU box).
+# -> build/ab/libdprf_<name>.so (run on the CPU side; the .so travels to the GPU box).  Goes through the
+# library's Makefile, so the per-object scheduler flags apply; override them through the environment
+# (make's ?= variables), e.g. SCHED_R6= tools/build_variant.sh r6_default
 set -e
 N=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/build/ab/$N
 mkdir -p $O
-for f in dprf_host.cpp dprf_kernels.hip dprf_kernels_r6.hip; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $R/dprf_amd/csrc/$f -o $O/${f%.*}.o &
-done
-wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/build/ab/libdprf_$N.so $O/*.o
+make -s -C $R/dprf_amd/csrc -j4 OUT=$R/build/ab/libdprf_$N.so OBJDIR=$O EXTRA="$*"
 echo $R/build/ab/libdprf_$N.so
