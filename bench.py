@@ -251,25 +251,42 @@ def run_workload(name, ctx, rank, world, steps, warmup, sync, allreduce_min, bat
     return dt, stats, lowest, pwlen
 
 
-def launch_traffic(path, workload, per_launch):
+def launch_traffic(path, workload, per_launch, build):
     """HBM bytes (FETCH_SIZE + WRITE_SIZE) of the dominant kernel per launch of THIS run: the profile's bytes
     per candidate x this run's candidates per launch (the adaptive chunking may size launches differently
-    from the profiled run); the profiled per-launch figure when the summary predates per-candidate bytes."""
+    from the profiled run).  Returns (bytes or None, record): the record names the profile and the build it
+    measured, and carries "stale": true when that build is not the library this run timed."""
     if not os.path.exists(path):
-        return None
-    tr = json.load(open(path)).get(workload, {})
+        return None, None
+    tr = json.load(open(path)).get(workload)
+    if not tr:
+        return None, None
+    rec = dict(tr, stale=tr.get("build") != build)
     if tr.get("bytes_per_candidate") is not None and per_launch:
-        return tr["bytes_per_candidate"] * per_launch
-    return tr.get("bytes_per_launch")
+        return tr["bytes_per_candidate"] * per_launch, rec
+    return tr.get("bytes_per_launch"), rec
 
 
-def pmc_summary(workload):
+def pmc_summary(workload, build):
     """rocprof-derived counters of the workload's dominant kernel (profiles/pmc_valu.json, written by
-    tools/pmc_valu.py from the tools/profile_gpu.sh passes): VALUBusy, VALUUtilization, LDS busy."""
+    tools/pmc_traffic.py from the tools/profile_gpu.sh passes): VALUBusy, VALUUtilization, LDS busy -- with the
+    build fingerprint of the library they were measured on and "stale": true when it is not this run's."""
     p = os.path.join(HERE, "profiles", "pmc_valu.json")
     if not os.path.exists(p):
         return None
-    return json.load(open(p)).get(workload)
+    rec = json.load(open(p)).get(workload)
+    return None if rec is None else dict(rec, stale=rec.get("build") != build)
+
+
+def device_balance(ctx):
+    """Per-device split of the last library call (dprf_ctx_last_call_devices) when this process drives several
+    GPUs through one context: candidates, launches, finish time, and the last device's finish over the mean."""
+    devs = ctx.last_call_devices()
+    if len(devs) < 2:
+        return None
+    fin = [d["finish_ms"] for d in devs]
+    mean = sum(fin) / len(fin)
+    return {"devices": devs, "last_over_mean": max(fin) / mean if mean > 0 else None}
 
 
 def summarize(stats, wkey, world, dt):
@@ -380,9 +397,11 @@ def main():
     dt_max = allreduce_max(dt)
     m = summarize(stats, wkey, world, dt_max)
     peak = work.PEAK_LANE_INSTR_PER_S
+    build = _lib.build_id()
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    traffic = launch_traffic(pmc, args.workload, m["per_launch"])
-    counters = pmc_summary(args.workload)
+    traffic, traffic_rec = launch_traffic(pmc, args.workload, m["per_launch"], build)
+    counters = pmc_summary(args.workload, build)
+    balance = device_balance(ctx)
 
     side = {}
     if not args.no_side:
@@ -404,12 +423,13 @@ def main():
             if work.BOUND.get(skey) == "lds":
                 side[name]["lds_cycle_frac"] = work.lds_frac(
                     skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
-            pc = pmc_summary(name)
+            pc = pmc_summary(name, build)
             if pc:
                 side[name]["rocprof"] = pc
-            tr = launch_traffic(pmc, name, sm["per_launch"])
+            tr, trec = launch_traffic(pmc, name, sm["per_launch"], build)
             if tr is not None:
                 side[name]["traffic_bytes_per_launch"] = tr
+                side[name]["traffic_source"] = {k: trec.get(k) for k in ("source", "build", "stale")}
             if name in side_cpu:
                 side[name]["cpu_baseline"] = side_cpu[name]
             sctx.close()
@@ -440,6 +460,9 @@ def main():
                 "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
                 "lds_cycle_frac": work.lds_frac(wkey, m["per_launch"] / (m["avg_launch_ms"] / 1e3)),
                 "call_overhead": m["call_overhead"]}
+        if traffic_rec:
+            roof["traffic_source"] = {k: traffic_rec.get(k) for k in ("source", "build", "stale", "fetch_bytes",
+                                                                      "write_bytes", "bytes_per_candidate")}
         if counters:
             roof["valu_busy"] = counters.get("valu_busy")
             roof["valu_utilization"] = counters.get("valu_utilization")
@@ -460,7 +483,7 @@ def main():
                     "reference's test document",
             "config": {"workload": args.workload, "description": desc, "document": stream_name,
                        "charset": "alnum (a-z A-Z 0-9)" if cs == ALNUM else "lowercase", "pwlen": pwlen,
-                       "batch_per_gpu": B, "kernel": ctx.kernel,
+                       "batch_per_gpu": B, "kernel": ctx.kernel, "build": build,
                        "parallelism": "keyspace shards x%d (%s)" % (
                            n_gpus, "one process per GPU" if dist else
                            "one process, %d-device library context" % len(devices))},
@@ -470,6 +493,8 @@ def main():
             "cluster": cluster,
             "lowest_hit_index": None if lowest is None or lowest >= (1 << 62) else lowest,
         }
+        if balance:
+            out["device_balance"] = balance
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

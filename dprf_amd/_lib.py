@@ -10,7 +10,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 ALL_DEVICES = -1
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
@@ -19,7 +19,8 @@ MAX_PW, MAX_PW_RANGE = 64, 32
 
 EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_device_list", "dprf_ctx_create",
            "dprf_ctx_create_devices", "dprf_ctx_destroy", "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel",
-           "dprf_ctx_devices", "dprf_search_range", "dprf_verify_list", "dprf_list_status"]
+           "dprf_ctx_devices", "dprf_search_range", "dprf_verify_list", "dprf_list_status", "dprf_build_id",
+           "dprf_plan_chunk", "dprf_ctx_last_call_devices"]
 
 
 class DprfError(RuntimeError):
@@ -32,6 +33,15 @@ class Stats(ctypes.Structure):
     _fields_ = [("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("devices", ctypes.c_uint32),
                 ("main_kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class DeviceStats(ctypes.Structure):
+    """dprf_device_stats (ABI 4): one device's share of the last call on a context."""
+    _fields_ = [("device", ctypes.c_int32), ("launches", ctypes.c_uint32), ("candidates", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double), ("first_ms", ctypes.c_double), ("finish_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -79,6 +89,12 @@ def lib():
                                            ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
             L.dprf_verify_list.restype = ctypes.c_int
+            L.dprf_build_id.restype = ctypes.c_char_p
+            L.dprf_plan_chunk.argtypes = [ctypes.c_char_p, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_int, ctypes.c_int]
+            L.dprf_plan_chunk.restype = ctypes.c_uint64
+            L.dprf_ctx_last_call_devices.argtypes = [ctypes.c_void_p, ctypes.POINTER(DeviceStats), ctypes.c_int]
+            L.dprf_ctx_last_call_devices.restype = ctypes.c_int
             if L.dprf_abi_version() != ABI_VERSION:
                 raise ImportError("libdprf.so ABI %d != %d" % (L.dprf_abi_version(), ABI_VERSION))
             _lib = L
@@ -92,6 +108,18 @@ def _check(rc):
 
 def device_count():
     return lib().dprf_device_count()
+
+
+def build_id():
+    """Fingerprint of the sources / flags / compiler libdprf.so was built from (dprf_build_id)."""
+    return lib().dprf_build_id().decode()
+
+
+def plan_chunk(kernel, rate_per_ms, remaining, total, ndev, inflight=0):
+    """The library's multi-device chunk policy (dprf_plan_chunk): a pure function, no device work.  0 = take
+    nothing now (scarce work and a launch still in flight), or an unknown kernel family."""
+    return int(lib().dprf_plan_chunk(kernel.encode(), float(rate_per_ms), int(remaining), int(total), int(ndev),
+                                     int(inflight)))
 
 
 def device_list():
@@ -157,6 +185,14 @@ class Context:
     @property
     def kernel(self):
         return lib().dprf_ctx_kernel(self._h).decode()
+
+    def last_call_devices(self):
+        """Per-device records of the last search/verify call (list of dicts, one per device)."""
+        arr = (DeviceStats * 64)()
+        n = lib().dprf_ctx_last_call_devices(self._h, arr, 64)
+        if n < 0:
+            _check(n)
+        return [arr[k].as_dict() for k in range(min(n, 64))]
 
     def search_range(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
         """Verify keyspace indices [start, start+count) of charset^pwlen (itertools.product order).

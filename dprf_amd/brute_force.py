@@ -40,7 +40,10 @@ ALNUM = LOWERCASE + LOWERCASE.upper() + "0123456789"   # the configs' "alnum" or
 DEFAULT_PASSWORD = "default_password_allocation"
 DUMMY = "_dummy"
 ROUND_SECONDS = 5.0              # range mode: wall time of one library call (checkpoint / Ctrl-C granularity)
-FIRST_ROUND = 1 << 22           # candidates of the first round, before a rate is known
+FIRST_ROUND = 1 << 22           # least candidates of the first round, before a rate is known
+ROUND_CHUNKS = 4                 # a round lasts at least this many of the library's largest chunks (0: fixed
+                                 # FIRST_ROUND / ROUND_SECONDS only)
+_HUGE = 1 << 62
 
 
 def init(stream, password_range, passwords, charset=LOWERCASE, devices=None, checkpoint=None):
@@ -119,10 +122,40 @@ class Checkpoint:
         os.replace(tmp, self.path)
 
 
-def next_round(rate, remaining, seconds=ROUND_SECONDS):
+def first_round(kernel, ndev):
+    """Candidates of the first range-mode round: ROUND_CHUNKS first chunks per device (the library's policy before
+    a rate is measured, dprf_plan_chunk), so no device idles in round 1 and its guided tail stays short."""
+    if not ROUND_CHUNKS or kernel is None:
+        return FIRST_ROUND
+    return max(FIRST_ROUND, ROUND_CHUNKS * ndev * _lib.plan_chunk(kernel, 0.0, _HUGE, _HUGE, 1))
+
+
+def round_seconds(kernel, rate, ndev):
+    """Wall time of one round at `rate` (cand/s over all devices): ROUND_SECONDS, or ROUND_CHUNKS times the
+    library's largest chunk at the per-device rate if that is longer, so the guided tail of a call (chunks
+    shrinking to the family's floor, include/dprf.h dprf_plan_chunk) stays a small part of the round."""
+    per_dev_ms = rate / 1e3 / max(1, ndev)
+    if per_dev_ms <= 0 or not ROUND_CHUNKS or kernel is None:
+        return ROUND_SECONDS
+    big = _lib.plan_chunk(kernel, per_dev_ms, _HUGE, _HUGE, 1)
+    return max(ROUND_SECONDS, ROUND_CHUNKS * big / per_dev_ms / 1e3)
+
+
+def next_round(rate, remaining, seconds=ROUND_SECONDS, first=FIRST_ROUND):
     """Candidates of the next range-mode round: ~`seconds` at the measured rate (cand/s; 0 = unknown)."""
-    n = FIRST_ROUND if rate <= 0 else max(FIRST_ROUND, int(rate * seconds))
+    n = first if rate <= 0 else max(first, int(rate * seconds))
     return min(remaining, n)
+
+
+def progress(t0, tried, remaining):
+    """The reference's progress report (brute_force.py:149-157: every 1000 candidates there, every round here):
+    running time, candidates tried, speed, and what is left to verify (the reference's queue size)."""
+    actual = time.time()
+    speed = tried / max(actual - t0, 1e-9)
+    print("Running time: " + str(actual - t0) + " & tried since: " + str(tried) + " passes")
+    print("Speed: " + str(speed) + " H/sec")
+    print("Queue size: " + str(remaining))
+    sys.stdout.flush()
 
 
 def search_round(ctx, charset, pwlen, start, count, stop_on_first=True):
@@ -160,8 +193,11 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
             print("Checkpoint: resuming at index %d" % done)
         space = len(charset) ** password_range
         found, rate = None, 0.0
+        ndev = len(getattr(ctx, "devices", [0]))
+        kernel = getattr(ctx, "kernel", None)
+        first = first_round(kernel, ndev)
         while done < space and found is None:
-            n = next_round(rate, space - done)
+            n = next_round(rate, space - done, round_seconds(kernel, rate, ndev), first)
             idx, st = search_round(ctx, charset, password_range, done, n)
             tried += st["candidates"]
             rate = st["candidates"] / max(st["wall_ms"] / 1e3, 1e-9)
@@ -169,6 +205,7 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
                 found = _index_to_password(idx, charset, password_range)
             done += n
             cp.save(done, found)
+            progress(t0, tried, space - done if found is None else 0)
         _report(found, tried, t0)
         return (1, found) if found is not None else (0, DEFAULT_PASSWORD)
     finally:

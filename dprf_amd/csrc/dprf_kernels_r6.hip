@@ -189,7 +189,8 @@ DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const ui
  * head of the lane's pattern column.  Returns the password length. */
 template <int MODE>
 DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, const uint8_t *sdig,
-                       uint64_t idx, const r6_lds &S, uint32_t K[16]) {
+                       uint64_t idx, uint32_t off, const uint32_t *slots, const uint8_t *lens, const r6_lds &S,
+                       uint32_t K[16]) {
     uint32_t w[DPRF_SLOT_WORDS];
 #pragma unroll
     for (int j = 0; j < DPRF_SLOT_WORDS; j++) w[j] = 0;
@@ -199,7 +200,7 @@ DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8
          * period column and the words read back: unrolled over DPRF_MAX_RANGE_LEN with the digits and the
          * words in registers, this once-per-candidate code spilled 300 B per lane in every wave of the
          * kernel (~2 KB of scratch writes per candidate, profiles/pmc_traffic.json r01) */
-        uint32_t rem = (uint32_t)(idx - e.start), carry = 0;
+        uint32_t rem = off, carry = 0;
         const uint32_t n = e.pwlen;
 #pragma unroll 1
         for (uint32_t k = 0; k < n; k++) {
@@ -222,13 +223,13 @@ DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8
         for (int j = 0; j < DPRF_SLOT_WORDS; j++)
             w[j] = 4u * (uint32_t)j < len ? *L32(S.pat + (((uint32_t)j << 8) | S.lanebase)) : 0u;
     } else {
-        const uint4 *s = (const uint4 *)(e.slots + idx * DPRF_SLOT_WORDS);
+        const uint4 *s = (const uint4 *)(slots + idx * DPRF_SLOT_WORDS);
 #pragma unroll
         for (int q = 0; q < DPRF_SLOT_WORDS / 4; q++) {
             uint4 v = s[q];
             w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
         }
-        len = e.lens[idx];
+        len = lens[idx];
     }
     /* K = SHA256(pw || salt8) (:240-245): LE message with the salt at byte offset len */
     uint32_t m[32];
@@ -436,7 +437,12 @@ struct r6_shared {
     uint32_t map[R6_CLASSES][R6_MAP_WORDS];   /* queued slots of each class, one bit per slot          */
     uint32_t count[R6_CLASSES];               /* queued slots per class (a hint for picking the class) */
     uint32_t live;                            /* slots holding a candidate                             */
-    uint32_t nslots, te_slots, pad;
+    uint32_t nslots, te_slots, ncand;
+    const uint32_t *slots;                    /* e.slots, e.lens (list mode), likewise */
+    const uint8_t *lens;
+    unsigned long long start;                 /* e.start / e.count (ncand) read from here when a slot takes or reports a
+                                                 candidate: kept in registers across the persistent loop, the
+                                                 64-bit start was spilled to scratch (SGPR pressure) */
     uint8_t sdig[DPRF_MAX_RANGE_LEN];         /* base-cslen digits of the launch's first index          */
     uint16_t stage[R6_LANES / 64][64];        /* per wave: the slot ids of the batch it claimed         */
     uint32_t state[R6_MAX_SLOTS];             /* len | bs << 8 | round << 16                            */
@@ -457,6 +463,11 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
     return S;
 }
 
+DEVI uint32_t lds_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+DEVI unsigned long long lds_load64(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int MODE>
 DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, dprf_results *R,
                    uint32_t stop_on_first, r6_shared *sh, const r6_lds &S, uint32_t slot) {
@@ -464,16 +475,16 @@ DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
      * been taken and will finish: skipping those above the lowest hit so far (stop_on_first) keeps the
      * reported hit the lowest of the call */
     uint32_t c = atomicAdd(&R->cursor, 1u);
-    if (c >= e.count) {
+    if (c >= lds_load(&sh->ncand)) {
         c = R6_IDLE;
-    } else if (stop_on_first && e.start + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    } else if (stop_on_first && lds_load64(&sh->start) + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         atomicAdd(&R->skipped, 1ull);
         c = R6_IDLE;
     }
     sh->cand[slot] = c;
     if (c == R6_IDLE) return false;
     uint32_t K[16];
-    const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, e.start + c, S, K);
+    const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, lds_load64(&sh->start) + c, c, sh->slots, sh->lens, S, K);
     r6_store_k(S, len, 32u, K);
     sh->state[slot] = len | (32u << 8);
     return true;
@@ -490,7 +501,6 @@ DEVI void r6_push(r6_shared *sh, const r6_lds &S, uint32_t slot) {
     atomicAdd(&sh->count[cls], 1u);
 }
 
-DEVI uint32_t lds_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
 /* Wave-uniform: claim up to 64 queued slots of the fullest class; returns how many (0: none queued) and
  * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
@@ -570,7 +580,13 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
     if (tid < R6_CLASSES) sh->count[tid] = 0u;
     if (tid < DPRF_MAX_RANGE_LEN) sh->sdig[tid] = e.sdig[tid];
-    if (tid == 0) sh->live = 0u;
+    if (tid == 0) {
+        sh->live = 0u;
+        sh->start = e.start;
+        sh->ncand = e.count;
+        sh->slots = e.slots;
+        sh->lens = e.lens;
+    }
     __syncthreads();
 
     for (uint32_t sl = tid; sl < nslots; sl += nthr) {
@@ -623,7 +639,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) ok = ok && K[kk] == p.u[kk];
                 if (ok) {
-                    const unsigned long long idx = e.start + sh->cand[slot];
+                    const unsigned long long idx = lds_load64(&sh->start) + sh->cand[slot];
                     uint32_t h = atomicAdd(&R->nhits, 1u);
                     if (h < cap) R->hits[h] = idx;
                     atomicMin(&R->first, idx);

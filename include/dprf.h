@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 3
+#define DPRF_ABI_VERSION 4
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -77,6 +77,17 @@ typedef struct dprf_stats {
 /* kernel_ms / main_kernel_ms are summed over the devices of a multi-device call (device time); wall_ms is
  * the call's wall time.  candidates / launches are totals over the devices. */
 
+/* Per-device record of the last dprf_search_range / dprf_verify_list call on a context (ABI 4): how the shared
+ * chunk cursor split the call, so imbalance between devices is visible (the sums above hide it). */
+typedef struct dprf_device_stats {
+    int32_t device;        /* HIP ordinal                                                              */
+    uint32_t launches;     /* chunks this device took                                                  */
+    uint64_t candidates;   /* candidates launched on it (before stop_on_first block skips)             */
+    double kernel_ms;      /* HIP-event device time of its launches                                    */
+    double first_ms;       /* host time from the call's start to its first launch                      */
+    double finish_ms;      /* host time from the call's start to when its last launch was retired      */
+} dprf_device_stats;
+
 /* ---- library ---- */
 int dprf_abi_version(void);
 const char *dprf_last_error(void);
@@ -84,6 +95,22 @@ int dprf_device_count(void);      /* gfx950 devices visible to this process */
 /* HIP ordinals of the visible gfx950 devices (a non-gfx950 device may sit at any ordinal): writes up to
  * cap ordinals, returns how many there are (ABI 3) */
 int dprf_device_list(int *ordinals, int cap);
+/* Fingerprint of the sources, Makefile flags and compiler this library was built from (ABI 4): bench.py prints
+ * it and tools/prof_summary.py records it, so a profile can be matched to the build it measured. */
+const char *dprf_build_id(void);
+/* The multi-device chunk policy as a pure function (ABI 4; no device work, usable without a GPU): the size of the
+ * next chunk a device of an `ndev`-device call takes from the shared cursor, for the kernel family `kernel`
+ * (dprf_ctx_kernel's names), the device's measured rate (candidates per device-ms, 0 = not measured yet), the
+ * candidates still unassigned (`remaining`) and the call's size (`total`).  A target-time size (a power of two,
+ * ~0.1-3 s of device time by family), capped for ndev > 1 at remaining / (4 ndev) -- guided self-scheduling over
+ * the two launches each device keeps in flight, so
+ * the chunks shrink as the call runs out and the devices finish together -- but not below the family's tail
+ * floor, nor below total / ndev for a call smaller than ndev floors (every device gets a share).  `inflight`: the
+ * device's launches still running; with ndev > 1 a device that has one does not take ahead while the remaining
+ * work is less than a chunk for every device -- the call returns 0 and the worker first waits for its launch.
+ * Returns 0 for an unknown family too. */
+uint64_t dprf_plan_chunk(const char *kernel, double rate_per_ms, uint64_t remaining, uint64_t total, int ndev,
+                         int inflight);
 
 /* ---- context: one document, one or more devices ----
  * fields/nfields: the array parse_verification_data() returns (brute_force.py:245-264), i.e. the
@@ -98,7 +125,10 @@ int dprf_ctx_devices(const dprf_ctx *ctx, int *ordinals, int cap);   /* returns 
 int dprf_ctx_destroy(dprf_ctx *ctx);
 int dprf_ctx_format(const dprf_ctx *ctx);
 int dprf_ctx_flags(const dprf_ctx *ctx);
-const char *dprf_ctx_kernel(const dprf_ctx *ctx);   /* kernel family name, e.g. "pdf_r34" */
+const char *dprf_ctx_kernel(const dprf_ctx *ctx);   /* kernel family name, e.g. "pdf_r24" */
+/* Per-device records of the context's last search / verify call (ABI 4): writes up to cap entries, returns the
+ * number of devices of that call (0 before the first call). */
+int dprf_ctx_last_call_devices(const dprf_ctx *ctx, dprf_device_stats *out, int cap);
 
 /* ---- range mode: brute_force.py -pr N (init_rangebased_brute_force :60-79, _generate :199-219) ----
  * Verifies candidates [start, start+count) of charset^pwlen in itertools.product order (leftmost

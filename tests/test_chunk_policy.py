@@ -1,0 +1,129 @@
+"""The multi-device chunk policy (include/dprf.h dprf_plan_chunk) on 8 simulated devices.
+
+The simulator mirrors a call of dprf_amd/csrc/dprf_host.cpp lane_run: every device keeps 2 launches in flight,
+retires the oldest when its ring is full (or when dprf_plan_chunk says work is too scarce to take ahead), then takes
+the next chunk from the shared cursor with the library's own
+dprf_plan_chunk (called through ctypes: the policy under test is the compiled one), and measures its rate from
+each retired launch.  Launch time = candidates / rate + a per-launch overhead (R6: its ~70 ms persistent-kernel
+drain, fitted to the round-2 launch-size measurements; others: 0.05 ms).  Rounds are sized the way
+brute_force's range mode sizes them (first_round / round_seconds / next_round), so the check covers the
+product's call pattern: in every round, round 1 included, the last device finishes within 5 % of the devices'
+mean finish time (tail imbalance; VERDICT r2 "guided chunking").
+CPU only: libdprf.so loads without a GPU and dprf_plan_chunk does no device work."""
+import heapq
+
+import pytest
+
+DEPTH = 2          # dprf_host.cpp MULTI_DEPTH (launches in flight per device in a multi-device call)
+# measured MI355X rates (profiles/bench_r02l.json), candidates per device-ms, and per-launch overhead ms
+RATES = {"pdf_r6": (3590.0, 70.0), "odf_aes256": (16400.0, 0.05), "pdf_r24": (565000.0, 0.05),
+         "office_std": (1370.0, 0.05), "pdf_r5": (30.3e6, 0.05)}
+
+
+def simulate_call(lib, kernel, total, rates, overhead, dev_rate):
+    """One library call over len(rates) devices; dev_rate: each device's measured rate carried between calls
+    (dev_lane::rate).  Returns per-device (finish_ms, candidates, launches)."""
+    nd = len(rates)
+    nxt = 0
+    queue = [[] for _ in range(nd)]        # (start, end, n) of launches in flight, oldest first
+    done = [0.0] * nd                      # when the device's stream is free
+    finish = [0.0] * nd
+    cands = [0] * nd
+    launches = [0] * nd
+    ev = [(0.0, d) for d in range(nd)]     # (host time the worker acts, device)
+    heapq.heapify(ev)
+    while ev:
+        t, d = heapq.heappop(ev)
+        if len(queue[d]) == DEPTH:         # retire the oldest (waits for it)
+            s, e, n = queue[d].pop(0)
+            t = max(t, e)
+            finish[d] = t
+            dev_rate[d] = n / (e - s)
+        if nxt >= total:
+            continue
+        want = lib.plan_chunk(kernel, dev_rate[d], total - nxt, total, nd, len(queue[d]))
+        if want == 0:                      # scarce work: retire the launch in flight first
+            s, e, n = queue[d].pop(0)
+            finish[d] = max(t, e)
+            dev_rate[d] = n / (e - s)
+            heapq.heappush(ev, (max(t, e), d))
+            continue
+        off = nxt
+        nxt += want
+        n = min(want, total - off)
+        s = max(t, done[d])
+        e = s + n / rates[d] + overhead
+        done[d] = e
+        queue[d].append((s, e, n))
+        cands[d] += n
+        launches[d] += 1
+        heapq.heappush(ev, (t if len(queue[d]) < DEPTH else queue[d][0][1], d))
+    for d in range(nd):                    # drain: retire whatever is still in flight
+        for s, e, n in queue[d]:
+            finish[d] = max(finish[d], e)
+            dev_rate[d] = n / (e - s)
+    return finish, cands, launches
+
+
+def run_search(lib, kernel, ndev, rounds, space=1 << 62, rate_spread=0.0):
+    from dprf_amd import brute_force as bf
+    base, overhead = RATES[kernel]
+    rates = [base * (1.0 - rate_spread * d / max(1, ndev - 1)) for d in range(ndev)]
+    dev_rate = [0.0] * ndev
+    rate, done, out = 0.0, 0, []
+    first = bf.first_round(kernel, ndev)
+    for _ in range(rounds):
+        n = bf.next_round(rate, space - done, bf.round_seconds(kernel, rate, ndev), first)
+        finish, cands, launches = simulate_call(lib, kernel, n, rates, overhead, dev_rate)
+        wall = max(finish)
+        assert sum(cands) == n
+        out.append({"n": n, "finish": finish, "cands": cands, "launches": launches, "wall_ms": wall})
+        rate = n / (wall / 1e3)
+        done += n
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from dprf_amd import _lib
+    try:
+        _lib.lib()
+    except ImportError as ex:
+        pytest.skip(str(ex))
+    return _lib
+
+
+@pytest.mark.parametrize("kernel", ["pdf_r6", "odf_aes256", "pdf_r24", "office_std", "pdf_r5"])
+def test_eight_devices_finish_together_in_every_round(lib, kernel):
+    for r, rd in enumerate(run_search(lib, kernel, 8, 4)):
+        mean = sum(rd["finish"]) / 8
+        assert max(rd["finish"]) <= 1.05 * mean, (kernel, r, rd)
+        assert min(rd["launches"]) >= 1, (kernel, r, rd)
+
+
+def test_uneven_devices_still_balance(lib):
+    """A device 20 % slower than the others (a throttled GPU) takes fewer chunks; the call still ends
+    together."""
+    for kernel in ("pdf_r6", "odf_aes256"):
+        for r, rd in enumerate(run_search(lib, kernel, 8, 3, rate_spread=0.2)):
+            mean = sum(rd["finish"]) / 8
+            assert max(rd["finish"]) <= 1.05 * mean, (kernel, r, rd)
+
+
+def test_small_call_spreads_over_every_device(lib):
+    """A client payload far smaller than one chunk (the first device used to take it all)."""
+    for kernel in RATES:
+        for n in (20000, 1 << 20):
+            finish, cands, launches = simulate_call(lib, kernel, n, [RATES[kernel][0]] * 8, 0.05, [0.0] * 8)
+            assert sum(cands) == n
+            assert min(cands) > 0, (kernel, n, cands)
+            assert max(cands) <= 2 * n / 8 + 4096, (kernel, n, cands)
+
+
+def test_single_device_policy_is_the_target_time_size(lib):
+    """ndev = 1: no guided cap, the power-of-two target-time chunk (unchanged from ABI 3)."""
+    assert lib.plan_chunk("pdf_r6", 0.0, 1 << 40, 1 << 40, 1) == 1 << 22
+    assert lib.plan_chunk("pdf_r6", 3590.0, 1 << 40, 1 << 40, 1) == 1 << 23
+    assert lib.plan_chunk("odf_aes256", 16400.0, 1 << 40, 1 << 40, 1) == 1 << 22
+    assert lib.plan_chunk("odf_aes256", 16400.0, 1000, 1 << 40, 1) == 1000
+    assert lib.plan_chunk("no_such_kernel", 1.0, 100, 100, 1) == 0

@@ -262,6 +262,7 @@ def test_multi_device_rounds_on_one_gpu(dprf, streams, monkeypatch):
     from dprf_amd import payload as pl
     monkeypatch.setattr(bf, "FIRST_ROUND", 4096)
     monkeypatch.setattr(bf, "ROUND_SECONDS", 0.0)
+    monkeypatch.setattr(bf, "ROUND_CHUNKS", 0)
     s = streams["pdf_synth_r3_l128_abc"]["stream"]
     for devs in ([0], [0, 0], [0, 0, 0]):
         assert bf.init(s, 3, None, devices=devs) == (1, "abc")
@@ -296,6 +297,32 @@ def test_multi_device_context_equals_one_device(dprf, streams):
             assert fst["candidates"] >= fh[0] - start + 1     # everything below the lowest hit was verified
             res[tuple(devs)] = hits
     assert res[(0,)] == res[(0, 0)]
+
+
+def test_small_call_spreads_over_every_device(dprf, streams):
+    """a call far smaller than a device's first chunk (a 20,000-candidate client payload; Office's first
+    chunk is 2^19) is split over every device of the context -- each lane of a {0,0,0,0} context launches at least
+    once (dprf_ctx_last_call_devices) -- with the same hits as one device."""
+    from dprf_amd import brute_force as bf
+    fields = bf.parse_verification_data(streams["office_testdoc"]["stream"])
+    rng = random.Random(9)
+    words = ["".join(rng.choice(LOWER) for _ in range(5)) for _ in range(20000)]
+    words[17001] = "password"
+    for devs in ([0], [0, 0, 0, 0]):
+        with dprf.Context(fields, devices=devs) as c:
+            hits, nh, st = c.verify_list(words)
+            assert hits == [17001] and st["candidates"] == len(words)
+            per = c.last_call_devices()
+            assert [d["device"] for d in per] == devs
+            assert all(d["launches"] >= 1 and d["candidates"] > 0 for d in per), per
+            assert sum(d["candidates"] for d in per) == len(words)
+            assert all(0 <= d["first_ms"] <= d["finish_ms"] for d in per), per
+    # range mode, a multi-launch call: the per-device records add up to the call
+    with dprf.Context(bf.parse_verification_data(streams["odt_testdoc_e"]["stream"]), devices=[0, 0]) as c:
+        _, _, st = c.search_range(ALNUM, 5, 0, 1 << 23)
+        per = c.last_call_devices()
+        assert sum(d["candidates"] for d in per) == 1 << 23 and sum(d["launches"] for d in per) == st["launches"]
+        assert all(d["launches"] >= 1 for d in per), per
 
 
 def test_concurrent_calls_on_one_context_are_serialised(dprf, streams):

@@ -136,3 +136,25 @@ def test_range_checkpoint_resumes_where_it_stopped(streams, oracle, tmp_path, mo
     assert bf.init_rangebased_brute_force(fields, 3, checkpoint=cp) == (1, "cat")
     with pytest.raises(ValueError):
         bf.init_rangebased_brute_force(fields, 4, checkpoint=cp)
+
+
+def test_range_mode_prints_progress_every_round(streams, oracle, monkeypatch, capsys):
+    """The reference prints running time, candidates tried, speed and queue size every 1000 candidates
+    (brute_force.py:149-157); range mode here prints the same three lines after every round,
+    and the answer is the same as without them."""
+    d = streams["pdf_synth_r5_cat"]
+    fields = bf.parse_verification_data(d["stream"])
+    monkeypatch.setattr(bf, "FIRST_ROUND", 1000)
+    monkeypatch.setattr(bf, "ROUND_SECONDS", 0.0)
+    log = []
+    monkeypatch.setattr(bf, "_context", lambda inp, dev: _OracleCtx(oracle, d["stream"], log))
+    capsys.readouterr()
+    assert bf.init_rangebased_brute_force(fields, 3) == (1, "cat")
+    out = capsys.readouterr().out.splitlines()
+    running = [ln for ln in out if ln.startswith("Running time: ")]
+    speed = [ln for ln in out if ln.startswith("Speed: ") and ln.endswith(" H/sec")]
+    queue = [ln for ln in out if ln.startswith("Queue size: ")]
+    assert len(running) == len(speed) == len(queue) == len(log) >= 2
+    tried = [int(ln.split("tried since: ")[1].split()[0]) for ln in running]
+    assert tried == [1 + sum(c for _, c in log[:k + 1]) for k in range(len(log))]   # + the "_dummy" candidate
+    assert int(queue[-1].split(": ")[1]) == 0 and int(queue[0].split(": ")[1]) == 26 ** 3 - 1000

@@ -283,3 +283,102 @@ def test_server_survives_a_client_that_dies_before_reading(streams):
     assert (found, sent) == (False, False)
     assert srv.clients == [] and "c1" not in srv.processed_passwords
     srv.pool.shutdown(wait=False)
+
+
+def _gpu_clients(port, hb, n, cwd):
+    """n real GPU client processes (python -m dprf_amd.client, one library context each on device 0), as
+    configs[4] runs them; returns their summary JSON lines."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, "-m", "dprf_amd.client", "127.0.0.1", str(port), "--devices", "0",
+                               "--heartbeat-port", str(hb), "--quiet"], cwd=cwd, env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for _ in range(n)]
+    out = []
+    for p in procs:
+        txt, _ = p.communicate(timeout=100)
+        lines = [ln for ln in txt.splitlines() if ln.startswith("{")]
+        assert lines, txt
+        out.append(json.loads(lines[-1]))
+    return out
+
+
+@pytest.mark.gpu
+def test_config5_two_gpu_clients_office_real_shape(tmp_path):
+    """configs[4] at its shape: an Office 2007 document written by tests/docgen.py whose
+    4-letter password sits in the last quarter of the server's lengths-1..4 order, served with -ps 65536 to TWO
+    GPU client processes on device 0.  The server's answer is the planted password; its global index in server
+    order is the planted one; both clients verified payloads; the oracle (the checker) accepts the password.
+    Uniqueness -- that no lower index also verifies -- is not re-derived on the CPU (475k Office verifies): the
+    check compares a 20-byte SHA-1 digest, so a second hit in the lower indices is a ~2^-141 event."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
+    import docgen
+    import pyoracle
+    from dprf_amd.parsers import office2john
+    pw = "uqyz"
+    ks = pl.Keyspace(pl.LOWERCASE, 4)
+    g = ks.global_index(pw)
+    assert g >= 3 * ks.total // 4
+    doc = str(tmp_path / "config5.docx")
+    docgen.write_docx(doc, pw, seed=5)
+    stream = office2john.get_hash(doc).strip()
+    assert pyoracle.Ctx(stream).verify(pw.encode())
+    srv = sv.Server(stream, password_range=4, payload_size=65536, heartbeat_port=_free_port(), quiet=True)
+    sent = []
+    orig = srv.handle_connection
+
+    def handle(client, address, message, segs):
+        r = orig(client, address, message, segs)
+        if r[1]:
+            sent.append(segs)
+        return r
+    srv.handle_connection = handle
+    th, out = _run_server(srv)
+    res = _gpu_clients(srv.address[1], srv.heartbeat_port, 2, os.path.dirname(os.path.dirname(__file__)))
+    th.join(30)
+    assert out["pw"] == pw and srv.found
+    assert ks.global_index(out["pw"]) == g
+    assert all(r["verified"] > 0 for r in res), res
+    assert sorted(r["password"] is not None for r in res) == [False, True], res
+    # payloads went out in server order and the one that holds g was among them
+    starts = [ks.global_index(ks.password(s[0][0], s[0][1])) for s in sent]
+    assert starts == sorted(starts)
+    assert any(st <= g < st + sum(c for _, _, c in s) for st, s in zip(starts, sent))
+
+
+@pytest.mark.gpu
+def test_config5_office_testdoc_first_mi_of_pr8_no_hit(streams):
+    """The reference's Office test document over the first 2^20 indices of the server's -pr 8 order (password
+    'password' lies at 129,052,722,139): no hit, and every payload verified exactly once by the two GPU
+    clients -- the server acknowledges 2^20 candidates, the clients' counts sum to 2^20, the payloads tile
+    [0, 2^20) without overlap."""
+    import os
+    s = streams["office_testdoc"]["stream"]
+    n = 1 << 20
+    srv = sv.Server(s, password_range=8, payload_size=65536, heartbeat_port=_free_port(), quiet=True,
+                    max_candidates=n)
+    sent = []
+    orig = srv.handle_connection
+
+    def handle(client, address, message, segs):
+        r = orig(client, address, message, segs)
+        if r[1]:
+            sent.append(segs)
+        return r
+    srv.handle_connection = handle
+    th, out = _run_server(srv)
+    res = _gpu_clients(srv.address[1], srv.heartbeat_port, 2, os.path.dirname(os.path.dirname(__file__)))
+    th.join(30)
+    assert out["pw"] is None and not srv.found
+    assert sum(r["verified"] for r in res) == n and all(r["verified"] > 0 for r in res), res
+    assert srv.counter == n
+    ks = pl.Keyspace(pl.LOWERCASE, 8)
+    spans = sorted((ks.global_index(ks.password(sg[0][0], sg[0][1])), sum(c for _, _, c in sg)) for sg in sent)
+    pos = 0
+    for st, c in spans:
+        assert st == pos
+        pos += c
+    assert pos == n

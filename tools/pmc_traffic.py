@@ -13,6 +13,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CUS, XCDS = 256, 8
 DOM = {"odt": "k_odt_kdf", "odt_e": "k_odt_kdf", "office": "k_office_kdf", "pdf_r34": "k_pdf_r24",
        "pdf_r2": "k_pdf_r24", "pdf_r5": "k_pdf_r5", "pdf_r6": "k_pdf_r6"}
 tags = sys.argv[1:] or ["r02"]
@@ -26,6 +27,7 @@ for w, kname in DOM.items():
     if f is None:
         continue
     d = json.load(open(f))
+    build = d.get("build")
     for k, v in d.get("counters", {}).items():
         if kname not in k:
             continue
@@ -35,12 +37,17 @@ for w, kname in DOM.items():
             traffic[w] = {"kernel": k, "bytes_per_launch": v.get("hbm_bytes_per_dispatch"),
                           "bytes_per_candidate": v.get("hbm_bytes_per_candidate"),
                           "fetch_bytes": pd.get("FETCH_SIZE", 0) * 1024, "write_bytes": pd.get("WRITE_SIZE", 0) * 1024,
-                          "source": src}
+                          "source": src, "build": build}
         if v.get("valu_busy") is not None:
             valu[w] = {"kernel": k, "valu_busy": v.get("valu_busy"), "valu_utilization": v.get("valu_utilization"),
                        "lds_busy": v.get("lds_busy"), "effective_clock_GHz": v.get("effective_clock_GHz"),
                        "valu_active_per_wave_cycle": v.get("valu_active_per_wave_cycle"),
-                       "SQ_LDS_BANK_CONFLICT_per_launch": pd.get("SQ_LDS_BANK_CONFLICT"), "source": src}
+                       "SQ_LDS_BANK_CONFLICT_per_launch": pd.get("SQ_LDS_BANK_CONFLICT"),
+                       # bank-conflict cycles (summed over the CUs) per CU cycle of the dispatch
+                       "lds_bank_conflict_frac": (pd["SQ_LDS_BANK_CONFLICT"] / (CUS * pd["GRBM_GUI_ACTIVE"] / XCDS)
+                                                  if pd.get("SQ_LDS_BANK_CONFLICT") is not None and pd.get("GRBM_GUI_ACTIVE")
+                                                  else None),
+                       "source": src, "build": build}
 for name, obj in (("pmc_traffic.json", traffic), ("pmc_valu.json", valu)):
     json.dump(obj, open(os.path.join(HERE, "profiles", name), "w"), indent=1)
 print(json.dumps({"traffic": traffic, "valu": valu}, indent=1))

@@ -60,6 +60,9 @@ def summarize(src, dst):
         except ValueError:
             pass
     bp = out.get("bench_under_profiler")
+    # the library build the profile measured (bench.py config.build = dprf_build_id()): bench.py marks counter
+    # fields taken from a different build "stale"
+    out["build"] = ((bp or {}).get("config") or {}).get("build")
     t = timed_dispatches(src, bp)
     if t:
         out["timed_kernel"] = t
