@@ -620,6 +620,15 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
 #ifndef R24_PRIO
 #define R24_PRIO 3
 #endif
+/* 1: the KSA as the generated asm block (rc4_dev.h rc4_ksa_asm); 0: the C++ rc4_ksa (A/B builds) */
+#ifndef R24_KSA_ASM
+#define R24_KSA_ASM 1
+#endif
+template <int NK>
+DEVI void r24_ksa(uint8_t *S, uint32_t sbase, uint32_t lane, const uint32_t k[4]) {
+    if (R24_KSA_ASM) rc4_ksa_asm<NK>(sbase, sbase + (lane << 2), k);
+    else rc4_ksa<NK>(S, lane << 2, k);
+}
 template <int R> struct r24_batches { static constexpr uint32_t v = R == 2 ? R2_BATCHES : R34_BATCHES; };
 template <int MODE, int R, int NK>
 __global__ void __launch_bounds__(128, 5)   /* 18 waves per CU (9 workgroups): <= 102 VGPRs */
@@ -678,6 +687,14 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     /* RC4 wave */
     __builtin_amdgcn_s_setprio(R24_PRIO);
     uint8_t *Sw = S;
+    /* the asm KSA needs the S-box area at an LDS address with zero low 16 bits (rc4_ksa_asm); S is this kernel's
+     * first LDS object, at 0 -- checked, and a launch that ever breaks it fails loudly instead of computing wrong */
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)S);
+    if (R24_KSA_ASM && (sbase & 0xffffu) != 0u) {
+        if (lane == 0) atomicOr(&R_->pad_, 2u);
+        for (uint32_t b = 0; b < nb; b++) { __syncthreads(); __syncthreads(); }   /* keep the key wave's barriers */
+        return;
+    }
 #pragma unroll 1
     for (uint32_t b = 0; b < nb; b++) {
         __syncthreads();
@@ -699,7 +716,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             uint32_t d[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) d[j] = p.pad[j];
-            rc4_ksa<5>(Sw, lane << 2, h);
+            r24_ksa<5>(Sw, sbase, lane, h);
             uint32_t jj = 0;
             rc4_prga_span<1, 4>(Sw, lane << 2, d, jj);
             if (__builtin_amdgcn_ballot_w64(valid && d[0] == p.u[0])) {
@@ -718,7 +735,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             for (uint32_t x = 0; x < 20u; x++) {
                 const uint32_t xx = x * 0x01010101u;
                 uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-                rc4_ksa<NK>(Sw, lane << 2, kx);
+                r24_ksa<NK>(Sw, sbase, lane, kx);
                 if (full) rc4_prga<16>(Sw, lane << 2, d);
                 else rc4_prga<2>(Sw, lane << 2, d);
             }

@@ -3,6 +3,7 @@
 #ifndef DPRF_RC4_DEV_H
 #define DPRF_RC4_DEV_H
 #include "dev_crypto.h"
+#include "rc4_ksa_asm.h"
 
 /* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
  * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave
@@ -103,6 +104,37 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
         x1 = hit ? x0 : x1;
         lds_st8(S, p0, hit ? v1 : x0);
         lds_st8(S, p0 + 1u, x1);
+    }
+}
+
+/* The same KSA as one generated inline-asm block (rc4_ksa_asm.h, tools/gen_rc4_ksa_asm.py: the schedule above in
+ * 11 VALU instructions per group of two steps instead of the 16-17 LLVM emits, byte selects as SDWA operands).
+ * sbase: LDS address of the wave's 16 KiB area, low 16 bits zero (the SDWA byte-1 insert of the S[j] address
+ * overwrites bits 8-15 of lanebase; the caller checks); lanebase = sbase + 4 * lane.  Writes the identity itself
+ * and returns with no LDS operation in flight. */
+template <int NK>
+DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
+    static_assert(NK == 5 || NK == 16, "rc4_ksa_asm.h holds the 5- and 16-byte key schedules");
+    uint32_t kb[NK];
+#pragma unroll
+    for (int q = 0; q < NK; q++) kb[q] = k[q >> 2] >> (8 * (q & 3));    /* only the low byte is used */
+    uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s;
+    if constexpr (NK == 16) {
+        asm volatile(RC4_KSA_ASM_16
+                     : "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st),
+                       "=&s"(m0s)
+                     : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1]), "v"(kb[2]), "v"(kb[3]), "v"(kb[4]),
+                       "v"(kb[(5) % NK]), "v"(kb[(6) % NK]), "v"(kb[(7) % NK]), "v"(kb[(8) % NK]), "v"(kb[(9) % NK]),
+                       "v"(kb[(10) % NK]), "v"(kb[(11) % NK]), "v"(kb[(12) % NK]), "v"(kb[(13) % NK]),
+                       "v"(kb[(14) % NK]), "v"(kb[(15) % NK])
+                     : "vcc", "memory");
+    } else {
+        asm volatile(RC4_KSA_ASM_5
+                     : "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st),
+                       "=&s"(m0s)
+                     : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1 % NK]), "v"(kb[2 % NK]), "v"(kb[3 % NK]),
+                       "v"(kb[4 % NK])
+                     : "vcc", "memory");
     }
 }
 

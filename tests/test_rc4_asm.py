@@ -1,0 +1,161 @@
+"""The generated RC4 key-schedule asm (dprf_amd/csrc/rc4_ksa_asm.h, tools/gen_rc4_ksa_asm.py) executed by a small
+emulator of the gfx950 instructions it uses, for a whole 64-lane wave with its 16 KiB S-box area, against a plain
+RC4 key schedule (RFC 6229's algorithm, the one EVP_rc4 runs for pdf_password_verifier.c:157-176).  This pins the
+schedule's dataflow -- deferred S[i] stores, SDWA byte selects, the [i/4][lane][i%4] layout -- on the CPU; the LDS
+wait placement is checked by construction in the generator (each consumer sits behind an lgkmcnt that covers its
+read) and on the GPU by the parity tests."""
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HDR = os.path.join(HERE, "..", "dprf_amd", "csrc", "rc4_ksa_asm.h")
+LANES = 64
+
+
+def program(nk):
+    text = open(HDR).read()
+    m = re.search(r"#define RC4_KSA_ASM_%d \\\n(.*?)\n    \"\"" % nk, text, re.S)
+    assert m, nk
+    return [ln.strip()[1:-len('\\n\\t" \\')] for ln in m.group(1).splitlines()]
+
+
+def ref_ksa(key, n):
+    S = list(range(256))
+    j = 0
+    for i in range(256):
+        j = (j + S[i] + key[i % n]) & 0xff
+        S[i], S[j] = S[j], S[i]
+    return S
+
+
+def emulate(prog, keys, nk, sbase=0):
+    """Run the block for 64 lanes; keys[l] = the lane's key bytes.  Returns the 64 S-boxes."""
+    lds = np.zeros(sbase + 16384, dtype=np.uint8)
+    lane = np.arange(LANES, dtype=np.uint64)
+    regs = {}
+    sregs = {"m0": 0}
+    kb = []
+    for q in range(nk):
+        w = np.array([int.from_bytes(bytes(k[(q & ~3):(q & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
+                     dtype=np.uint64)
+        kb.append(w >> np.uint64(8 * (q & 3)))            # garbage above byte 0, as the kernel passes them
+    vin = {"%10": sbase + 4 * lane, "%11": sbase}
+    for q in range(nk):
+        vin["%%%d" % (12 + q)] = kb[q]
+    vcc = np.zeros(LANES, dtype=bool)
+    M32 = np.uint64(0xffffffff)
+
+    def v(x):
+        if x in vin and not isinstance(vin[x], int):
+            return vin[x]
+        if x in regs:
+            return regs[x]
+        if x.startswith("0x") or x.isdigit():
+            return np.full(LANES, int(x, 0), dtype=np.uint64)
+        raise KeyError(x)
+
+    def s(x):
+        if x == "m0":
+            return sregs["m0"]
+        if x in vin and isinstance(vin[x], int):
+            return vin[x]
+        if x in sregs:
+            return sregs[x]
+        return int(x, 0)
+
+    def off(tok):
+        return int(tok.split(":")[1]) if tok and tok.startswith("offset:") else 0
+
+    for ln in prog:
+        op, _, rest = ln.partition(" ")
+        a = [t.strip() for t in rest.split(",")]
+        last = a[-1].split() if a else []
+        if op == "s_mov_b32":
+            sregs[a[0]] = s(a[1])
+        elif op == "s_movk_i32":
+            sregs[a[0]] = int(a[1], 0)
+        elif op == "s_waitcnt":
+            pass
+        elif op == "v_mov_b32":
+            regs[a[0]] = v(a[1]).copy()
+        elif op == "ds_write_addtid_b32":
+            d, o = a[0].split()[0], off(a[0].split()[1])
+            for l_ in range(LANES):
+                addr = sregs["m0"] + o + 4 * l_
+                lds[addr:addr + 4] = np.frombuffer(int(v(d)[l_]).to_bytes(4, "little"), dtype=np.uint8)
+        elif op == "v_add_u32":
+            regs[a[0]] = (v(a[1]) + v(a[2])) & M32
+        elif op == "v_add3_u32":
+            regs[a[0]] = (v(a[1]) + v(a[2]) + v(a[3])) & M32
+        elif op == "v_and_or_b32":
+            regs[a[0]] = (v(a[1]) & v(a[2])) | v(a[3])
+        elif op == "v_lshrrev_b32_sdwa":
+            assert "dst_sel:BYTE_1" in ln and "UNUSED_PRESERVE" in ln and "src1_sel:BYTE_0" in ln
+            src = v(a[2].split()[0]) & np.uint64(0xff)
+            shifted = (src >> np.uint64(int(a[1]))) & np.uint64(0xff)
+            regs[a[0]] = (regs[a[0]] & ~np.uint64(0xff00) & M32) | (shifted << np.uint64(8))
+        elif op == "v_cmp_eq_u32_sdwa":
+            assert a[0] == "vcc" and "src0_sel:BYTE_0" in ln
+            vcc = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(a[2].split()[0]))
+        elif op == "ds_read_u8":
+            regs[a[0]] = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
+        elif op == "ds_write_b8":
+            lds[v(a[0]).astype(np.int64)] = (v(a[1]) & np.uint64(0xff)).astype(np.uint8)
+        elif op == "ds_read_u16":
+            base, o = a[1].split()[0], off(a[1].split()[1])
+            ad = (v(base) + np.uint64(o)).astype(np.int64)
+            regs[a[0]] = lds[ad].astype(np.uint64) | (lds[ad + 1].astype(np.uint64) << np.uint64(8))
+        elif op == "ds_write_b16":
+            d, o = a[1].split()[0], off(a[1].split()[1])
+            ad = (v(a[0]) + np.uint64(o)).astype(np.int64)
+            val = v(d)
+            lds[ad] = (val & np.uint64(0xff)).astype(np.uint8)
+            lds[ad + 1] = ((val >> np.uint64(8)) & np.uint64(0xff)).astype(np.uint8)
+        elif op == "v_cndmask_b32_e32":
+            regs[a[0]] = np.where(vcc, v(a[2]), v(a[1]))
+        elif op == "v_cndmask_b32_sdwa":
+            s0, s1 = v(a[1]), v(a[2])
+            sel = {"DWORD": (0, 0xffffffff), "BYTE_0": (0, 0xff), "BYTE_1": (8, 0xff)}
+            sh0, m0_ = sel[re.search(r"src0_sel:(\w+)", ln).group(1)]
+            sh1, m1_ = sel[re.search(r"src1_sel:(\w+)", ln).group(1)]
+            r = np.where(vcc, (s1 >> np.uint64(sh1)) & np.uint64(m1_), (s0 >> np.uint64(sh0)) & np.uint64(m0_))
+            if "dst_sel:BYTE_1" in ln:
+                assert "UNUSED_PRESERVE" in ln
+                regs[a[0]] = (regs[a[0]] & ~np.uint64(0xff00) & M32) | ((r & np.uint64(0xff)) << np.uint64(8))
+            else:
+                assert "dst_sel:DWORD" in ln
+                regs[a[0]] = r
+        else:
+            raise AssertionError("instruction the emulator does not know: " + ln)
+    out = []
+    for l_ in range(LANES):
+        out.append([int(lds[sbase + ((i >> 2) << 8) + 4 * l_ + (i & 3)]) for i in range(256)])
+    return out
+
+
+@pytest.mark.parametrize("nk", [5, 16])
+def test_generated_ksa_equals_rc4(nk):
+    if not os.path.exists(HDR):
+        pytest.skip("rc4_ksa_asm.h not generated")
+    prog = program(nk)
+    rng = random.Random(nk)
+    for trial in range(3):
+        keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
+        if trial == 1:
+            keys[0] = [0] * 16                     # j == i collisions early on
+            keys[1] = [1] * 16
+        got = emulate(prog, keys, nk)
+        for l_ in range(LANES):
+            assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
+
+
+def test_header_is_what_the_generator_writes():
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    out = subprocess.run([sys.executable, gen], capture_output=True, text=True, check=True).stdout
+    assert out == open(HDR).read()

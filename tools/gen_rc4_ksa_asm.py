@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Generate dprf_amd/csrc/rc4_ksa_asm.h: the RC4 key schedule of the PDF R2-R4 kernels as one gfx950 inline-asm
+block per key length (pdf_password_verifier.c:157-176 via EVP_rc4; RC4 itself: S = identity, then for i = 0..255
+j += S[i] + K[i % n]; swap(S[i], S[j])).
+
+Why asm: the compiled C++ schedule (rc4_dev.h rc4_ksa) issues 16-17 VALU instructions per group of two steps
+(~31 issue slots: byte extracts, compare + select pairs, a u16 merge in two steps); the same dataflow fits in 11,
+~21 slots, with the byte selects folded into SDWA operands -- and only asm keeps LLVM from re-materialising or
+re-ordering them.  The schedule is rc4_ksa's group-deferred one (rc4_dev.h): per group q (i0 = 2q, i1 = 2q + 1)
+
+    wait for W = S[i0] | S[i1] << 8            (read at the end of group q - 1; lgkmcnt(1): the u16 store
+                                                 issued after it may stay in flight -- LDS completes in order)
+    j += W + K[i0]                              (only j's low byte is ever used: W's byte 1 above it is harmless)
+    a0 = (j & 3) | lanebase; a0.byte1 = j.byte0 >> 2            -> address of S[j] in the [i/4][lane][i%4] layout
+    hit1 = (j.byte0 == i1)
+    x0 = S[j]; S[j] = W.byte0
+    v1 = hit1 ? W.byte0 : W.byte1               (one SDWA cndmask: the current S[i1])
+    j += v1 + K[i1];  a1 likewise;  hit0 = (j.byte0 == i0)
+    x1 = S[j]; S[j] = v1
+    W = S[i0 + 2] | S[i0 + 3] << 8              (after both S[j] stores, before the deferred S[i] stores)
+    wait for x0, x1 (lgkmcnt(1))
+    m = hit0 ? v1 : x0;  m.byte1 = hit0 ? x0 : x1                -> S[i0], S[i1] as one u16
+    store m at S[i0]
+
+Hazards: every VCC consumer (v_cndmask) is at least two instructions after the v_cmp that writes VCC (the LDS
+instructions in between count as wait states).  The block writes the identity itself (ds_write_addtid_b32 through
+M0, restored at the end) and ends with lgkmcnt(0), so the compiler never sees an LDS operation of this block in
+flight.  Requirements (checked by the caller): the S-box area starts at an LDS address whose low 16 bits are zero
+(the SDWA byte-1 insert overwrites bits 8-15 of lanebase) and lanebase = area + 4 * lane.
+
+Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
+"""
+
+KEYLENS = (5, 16)   # R2 / R3-R4 with 40-bit keys use 5 bytes, R3/R4 128-bit keys 16 (EVP_rc4 reads 16)
+
+
+def pos(i):
+    """byte offset of S[i] from the lane's column base"""
+    return ((i >> 2) << 8) + (i & 3)
+
+
+def ksa(nk):
+    # operands: %0 j (in/out), %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR),
+    #           %10 lanebase, %11 sbase (SGPR, the area's LDS address for ds_write_addtid), %12.. key bytes
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, LB, SB = ("%%%d" % k for k in range(12))
+    KB = ["%%%d" % (12 + k) for k in range(nk)]
+    out = []
+    e = out.append
+    # identity: dword w of lane l at area + 256 w + 4 l = M0 + offset + 4 * lane
+    e("s_mov_b32 %s, m0" % M0S)
+    e("s_mov_b32 m0, %s" % SB)
+    e("v_mov_b32 %s, 0x3020100" % M)
+    for w in range(64):
+        e("ds_write_addtid_b32 %s offset:%d" % (M, 256 * w))
+        if w < 63:
+            e("v_add_u32 %s, 0x4040404, %s" % (M, M))
+    e("s_mov_b32 m0, %s" % M0S)
+    e("v_mov_b32 %s, 0" % J)
+    e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
+    for q in range(128):
+        i0, i1 = 2 * q, 2 * q + 1
+        if q > 0:
+            e("s_waitcnt lgkmcnt(1)")
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
+        e("s_movk_i32 %s, %d" % (ST, i1))
+        e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A0, J))
+        e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        e("ds_read_u8 %s, %s" % (X0, A0))
+        e("ds_write_b8 %s, %s" % (A0, W))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
+          % (V1, W, W))
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
+        e("s_movk_i32 %s, %d" % (ST, i0))
+        e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A1, J))
+        e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        e("ds_read_u8 %s, %s" % (X1, A1))
+        e("ds_write_b8 %s, %s" % (A1, V1))
+        if q < 127:
+            e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
+            e("s_waitcnt lgkmcnt(1)")
+        else:
+            e("s_waitcnt lgkmcnt(0)")
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+          % (M, X1, X0))
+        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(i0)))
+    e("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def main():
+    print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
+    print("#ifndef DPRF_RC4_KSA_ASM_H")
+    print("#define DPRF_RC4_KSA_ASM_H")
+    for nk in KEYLENS:
+        lines = ksa(nk)
+        print("#define RC4_KSA_ASM_%d \\" % nk)
+        for ln in lines:
+            print('    "%s\\n\\t" \\' % ln)
+        print('    ""')
+    print("#endif")
+
+
+if __name__ == "__main__":
+    main()

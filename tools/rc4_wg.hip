@@ -2,6 +2,7 @@
  * and what the product KSA (rc4_dev.h) gains from the 10th one.
  *   A  one wave per workgroup, 16 KiB each (the LDS allocator gives 9 per CU)
  *   B  one 640-thread workgroup per CU declaring all 160 KiB: 10 RC4 waves, persistent over the batches
+ *   A' A with the generated asm KSA (rc4_ksa_asm.h); same checksum required
  *   C  B + 4 key waves per workgroup doing dummy VALU work (MD5 x51) and a barrier pair per batch, as the
  *      product's key/RC4 split would
  * Each candidate: 20 x (KSA with a 16-byte key + the 2-byte early-reject PRGA); all variants must give the
@@ -16,18 +17,25 @@
 
 DEVI uint32_t mix(uint32_t x) { x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x; }
 
+template <bool ASM = false>
 DEVI uint32_t one_candidate(uint8_t *S, uint32_t lanebase, uint32_t g) {
     uint32_t h[4] = {mix(g), mix(g ^ 0x1111u), mix(g ^ 0x2222u), mix(g ^ 0x3333u)};
     uint32_t d[4] = {0x01234567u, 0, 0, 0};
     for (uint32_t x = 0; x < 20u; x++) {
         const uint32_t xx = x * 0x01010101u;
         uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-        rc4_ksa<16>(S, lanebase, kx);
+        if (ASM) {
+            const uint32_t sb = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)S;
+            rc4_ksa_asm<16>(sb, sb + lanebase, kx);
+        } else {
+            rc4_ksa<16>(S, lanebase, kx);
+        }
         rc4_prga<2>(S, lanebase, d);
     }
     return d[0] & 0xffffu;
 }
 
+template <bool ASM>
 __global__ void __launch_bounds__(64) k_a(uint32_t nb, unsigned long long *sum) {
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
     __builtin_amdgcn_s_setprio(3);
@@ -35,7 +43,7 @@ __global__ void __launch_bounds__(64) k_a(uint32_t nb, unsigned long long *sum) 
     unsigned long long acc = 0;
     for (uint32_t b = 0; b < nb; b++) {
         const uint32_t g = (blockIdx.x * nb + b) * 64u + lane;
-        acc += (unsigned long long)one_candidate(S, lane << 2, g) * (g | 1u);
+        acc += (unsigned long long)one_candidate<ASM>(S, lane << 2, g) * (g | 1u);
     }
     atomicAdd(sum, acc);
 }
@@ -91,13 +99,14 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 5; v++) {
         float best = 1e30f;
         unsigned long long h = 0;
         for (int r = 0; r < reps; r++) {
             CHECK(hipMemset(sum, 0, 8));
             CHECK(hipEventRecord(e0));
-            if (v == 0) hipLaunchKernelGGL(k_a, dim3(nwb / 8), dim3(64), 0, 0, 8u, sum);
+            if (v == 0) hipLaunchKernelGGL(k_a<false>, dim3(nwb / 8), dim3(64), 0, 0, 8u, sum);
+            else if (v == 4) hipLaunchKernelGGL(k_a<true>, dim3(nwb / 8), dim3(64), 0, 0, 8u, sum);
             else if (v == 1) hipLaunchKernelGGL(k_b<0>, dim3(cus), dim3(640), 0, 0, nwb, sum, sink);
             else if (v == 2) hipLaunchKernelGGL(k_b<5>, dim3(cus), dim3(640 + 320), 0, 0, nwb, sum, sink);
             else hipLaunchKernelGGL(k_b<2>, dim3(cus), dim3(640 + 128), 0, 0, nwb, sum, sink);
@@ -110,7 +119,7 @@ int main(int argc, char **argv) {
             CHECK(hipMemcpy(&h, sum, 8, hipMemcpyDeviceToHost));
         }
         static const char *name[] = {"A 1 wave/WG (9 per CU)", "B 10 RC4 waves, 160 KiB WG", "C B + 5 key waves, barriers",
-                                     "C' B + 2 key waves, barriers"};
+                                     "C' B + 2 key waves, barriers", "A with the asm KSA (rc4_ksa_asm.h)"};
         printf("%-32s %9.3f ms  %7.1f M cand/s  checksum %016llx\n", name[v], best, n / (best * 1e3), h);
     }
     return 0;
