@@ -278,6 +278,16 @@ def pmc_summary(workload, build):
     return None if rec is None else dict(rec, stale=rec.get("build") != build)
 
 
+def measured_bound(counters, wkey):
+    """The dominant kernel's binding pipe from its rocprof counters of THIS build: "lds" when the LDS array is
+    busier (ROCm LdsUtil, SQ_LDS_IDX_ACTIVE) than the SIMDs issue VALU (VALUBusy), else "valu".  Falls back to
+    dprf_amd/work.py's static BOUND when no current profile has the counters (source says which)."""
+    from dprf_amd import work
+    if counters and not counters.get("stale") and counters.get("lds_util") is not None and counters.get("valu_busy"):
+        return ("lds" if counters["lds_util"] > counters["valu_busy"] else "valu"), "rocprof"
+    return work.BOUND.get(wkey, "valu"), "model"
+
+
 def device_balance(ctx):
     """Per-device split of the last library call (dprf_ctx_last_call_devices) when this process drives several
     GPUs through one context: candidates, launches, finish time, and the last device's finish over the mean."""
@@ -415,7 +425,7 @@ def main():
             sdt = allreduce_max(sdt)
             sm = summarize(sst, skey, world, sdt)
             side[name] = {"value": sm["value"], "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
-                          "pwlen": spl, "bound": work.BOUND.get(skey, "valu"),
+                          "pwlen": spl, "bound": measured_bound(pmc_summary(name, build), skey)[0],
                           "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
                           "valu_floor_frac": (sm["per_launch"] * work.per_candidate(skey)
                                               / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak),
@@ -449,7 +459,8 @@ def main():
             cluster = {"error": repr(ex)}
 
     if rank == 0:
-        roof = {"bound": work.BOUND.get(wkey, "valu"), "achieved": m["achieved"] / 1e12, "peak": peak / 1e12,
+        bound, bound_src = measured_bound(counters, wkey)
+        roof = {"bound": bound, "bound_source": bound_src, "achieved": m["achieved"] / 1e12, "peak": peak / 1e12,
                 "unit": "T VALU lane-slots/s (gfx950 issue-slot floor of the algorithm)",
                 "frac": m["achieved"] / peak, "traffic": traffic,
                 "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),

@@ -3,7 +3,11 @@
 #ifndef DPRF_RC4_DEV_H
 #define DPRF_RC4_DEV_H
 #include "dev_crypto.h"
+#ifdef RC4_KSA_ASM_HEADER            /* A/B builds: a variant of the generated schedule */
+#include RC4_KSA_ASM_HEADER
+#else
 #include "rc4_ksa_asm.h"
+#endif
 
 /* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
  * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave

@@ -29,6 +29,9 @@ flight.  Requirements (checked by the caller): the S-box area starts at an LDS a
 (the SDWA byte-1 insert overwrites bits 8-15 of lanebase) and lanebase = area + 4 * lane.
 
 Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
+       tools/gen_rc4_ksa_asm.py --early-read > <variant header>   (A/B: each S[j] read one instruction earlier)
+       tools/gen_rc4_ksa_asm.py --late-merge > <variant header>   (A/B: group q-1's S[i] merge + store issued
+                                                                    inside group q, between a0 and the S[j] read)
 """
 
 KEYLENS = (5, 16)   # R2 / R3-R4 with 40-bit keys use 5 bytes, R3/R4 128-bit keys 16 (EVP_rc4 reads 16)
@@ -39,7 +42,7 @@ def pos(i):
     return ((i >> 2) << 8) + (i & 3)
 
 
-def ksa(nk):
+def ksa(nk, early_read=False, late_merge=False):
     # operands: %0 j (in/out), %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR),
     #           %10 lanebase, %11 sbase (SGPR, the area's LDS address for ds_write_addtid), %12.. key bytes
     J, W, X0, X1, V1, A0, A1, M, ST, M0S, LB, SB = ("%%%d" % k for k in range(12))
@@ -57,47 +60,74 @@ def ksa(nk):
     e("s_mov_b32 m0, %s" % M0S)
     e("v_mov_b32 %s, 0" % J)
     e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
+    def merge(q):
+        """the deferred S[i0], S[i1] of group q as one u16 (VCC = hit0 of group q)"""
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+          % (M, X1, X0))
+        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(2 * q)))
+
     for q in range(128):
         i0, i1 = 2 * q, 2 * q + 1
         if q > 0:
-            e("s_waitcnt lgkmcnt(1)")
+            e("s_waitcnt lgkmcnt(%d)" % (0 if late_merge else 1))
         e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
         e("s_movk_i32 %s, %d" % (ST, i1))
         e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
           % (A0, J))
-        e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
-        e("ds_read_u8 %s, %s" % (X0, A0))
-        e("ds_write_b8 %s, %s" % (A0, W))
+        if late_merge and q > 0:
+            merge(q - 1)    # its S[i] stores precede this group's S[j] read (LDS in order), VCC still hit0(q-1)
+        if early_read:      # the S[j] read one instruction earlier; the SALU move keeps the VCC distance
+            e("ds_read_u8 %s, %s" % (X0, A0))
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+            e("ds_write_b8 %s, %s" % (A0, W))
+            e("s_movk_i32 %s, %d" % (ST, i0))
+        else:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+            e("ds_read_u8 %s, %s" % (X0, A0))
+            e("ds_write_b8 %s, %s" % (A0, W))
         e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
           % (V1, W, W))
         e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
-        e("s_movk_i32 %s, %d" % (ST, i0))
+        if not early_read:
+            e("s_movk_i32 %s, %d" % (ST, i0))
         e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
           % (A1, J))
-        e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
-        e("ds_read_u8 %s, %s" % (X1, A1))
+        if early_read:
+            e("ds_read_u8 %s, %s" % (X1, A1))
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        else:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+            e("ds_read_u8 %s, %s" % (X1, A1))
         e("ds_write_b8 %s, %s" % (A1, V1))
+        if late_merge:
+            if q < 127:
+                e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
+            else:
+                e("s_waitcnt lgkmcnt(0)")
+                merge(q)
+            continue
         if q < 127:
             e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
             e("s_waitcnt lgkmcnt(1)")
         else:
             e("s_waitcnt lgkmcnt(0)")
-        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
-        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-          % (M, X1, X0))
-        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(i0)))
+        merge(q)
     e("s_waitcnt lgkmcnt(0)")
     return out
 
 
 def main():
+    import sys
+    early = "--early-read" in sys.argv      # A/B variants (tools/build_variant.sh with RC4_KSA_ASM_HEADER)
+    late = "--late-merge" in sys.argv
     print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
     print("#ifndef DPRF_RC4_KSA_ASM_H")
     print("#define DPRF_RC4_KSA_ASM_H")
     for nk in KEYLENS:
-        lines = ksa(nk)
+        lines = ksa(nk, early, late)
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)

@@ -40,7 +40,8 @@ for w, kname in DOM.items():
                           "source": src, "build": build}
         if v.get("valu_busy") is not None:
             valu[w] = {"kernel": k, "valu_busy": v.get("valu_busy"), "valu_utilization": v.get("valu_utilization"),
-                       "lds_busy": v.get("lds_busy"), "effective_clock_GHz": v.get("effective_clock_GHz"),
+                       "lds_busy": v.get("lds_busy"), "lds_util": v.get("lds_util"),
+                       "effective_clock_GHz": v.get("effective_clock_GHz"),
                        "valu_active_per_wave_cycle": v.get("valu_active_per_wave_cycle"),
                        "SQ_LDS_BANK_CONFLICT_per_launch": pd.get("SQ_LDS_BANK_CONFLICT"),
                        # bank-conflict cycles (summed over the CUs) per CU cycle of the dispatch

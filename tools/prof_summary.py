@@ -9,6 +9,7 @@ each kernel, and the derived metrics are computed within one pass:
                      MI355X_MICROARCH.md)
   valu_utilization = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)           (ROCm's VALUUtilization)
   lds_busy         = SQ_ACTIVE_INST_LDS * 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs)    (same form, LDS instructions)
+  lds_util         = SQ_LDS_IDX_ACTIVE / CUs / (GRBM_GUI_ACTIVE / XCDs)            (ROCm's LdsUtil: LDS-array cycles)
   effective_clock  = GRBM_GUI_ACTIVE / XCDs / kernel duration
 HBM bytes are also given per candidate (each PMC pass runs bench.py --steps 1 --warmup 0, i.e. exactly one
 batch of candidates, whatever launch sizes the adaptive chunking chose), so bench.py can scale them to its own
@@ -22,7 +23,7 @@ import os
 import shutil
 import sys
 
-SIMDS, XCDS = 256 * 4, 8
+SIMDS, XCDS, CUS = 256 * 4, 8, 256
 PASSES = ("fetch", "write", "sq", "lds")
 PMC_STEPS = 1          # tools/profile_gpu.sh: --steps 1 --warmup 0 for every --pmc pass
 
@@ -98,6 +99,12 @@ def summarize(src, dst):
                     per["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / cyc
                 if "SQ_ACTIVE_INST_LDS" in avg:
                     per["lds_busy"] = avg["SQ_ACTIVE_INST_LDS"] * 4 / SIMDS / cyc
+                if "SQ_LDS_IDX_ACTIVE" in avg:
+                    # ROCm's LdsUtil: LDS-array cycles of indexed operations over the CUs' cycles (the fraction of
+                    # the LDS pipeline in use; SQ_ACTIVE_INST_LDS above counts instruction issue on the SIMDs)
+                    per["lds_util"] = avg["SQ_LDS_IDX_ACTIVE"] / (CUS * cyc)
+                if "SQ_LDS_BANK_CONFLICT" in avg:
+                    per["lds_bank_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / (CUS * cyc)
             if avg.get("SQ_THREAD_CYCLES_VALU") and avg.get("SQ_ACTIVE_INST_VALU"):
                 per["valu_utilization"] = avg["SQ_THREAD_CYCLES_VALU"] / (avg["SQ_ACTIVE_INST_VALU"] * 64)
             if avg.get("SQ_ACTIVE_INST_VALU") and avg.get("SQ_WAVE_CYCLES"):
