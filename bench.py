@@ -355,7 +355,10 @@ def main():
     # one process through one multi-device library context instead
     devices = [local]
     if world == 1 and args.gpus > 1:
-        devices = _lib.device_list()[:args.gpus]
+        if os.environ.get("DPRF_BENCH_SAME_DEVICE") == "1":
+            devices = [local] * args.gpus        # rehearsal: N library lanes (threads + streams) on one GPU
+        else:
+            devices = _lib.device_list()[:args.gpus]
         if len(devices) < args.gpus:
             raise SystemExit("--gpus %d: only %d gfx950 devices visible" % (args.gpus, len(devices)))
 

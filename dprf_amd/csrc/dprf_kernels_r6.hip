@@ -471,14 +471,7 @@ DEVI unsigned long long lds_load64(const unsigned long long *p) {
 /* Candidate numbers for the active lanes that ask (need): ONE atomicAdd on the launch's cursor per wave, each
  * asking lane gets base + its rank among them (ids stay in increasing lane order).  A per-lane atomic made every
  * candidate start a device-scope atomic: ~31 B of HBM writes per candidate (profiles/prof_pdf_r6_r03a.json). */
-#ifndef R6_TAKE_AGG
-#define R6_TAKE_AGG 1
-#endif
-#ifndef R6_LANE_MAP
-#define R6_LANE_MAP 1
-#endif
 DEVI uint32_t r6_take(dprf_results *R, bool need, uint32_t lane) {
-    if (!R6_TAKE_AGG) return need ? atomicAdd(&R->cursor, 1u) : R6_IDLE;
     const uint64_t m = __builtin_amdgcn_ballot_w64(need);
     if (m == 0) return R6_IDLE;
     const uint32_t leader = (uint32_t)__builtin_ctzll(m);
@@ -557,70 +550,24 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
         }
     }
     const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
-    if (!R6_LANE_MAP) {
-        const uint32_t ng = __builtin_popcount(got);
-        uint32_t off = ng;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(off, d, 64);
-            if (lane >= (uint32_t)d) off += o;
-        }
-        const uint32_t total = __builtin_amdgcn_readlane(off, 63);
-        off -= ng;
-        for (uint32_t b = got; b; b &= b - 1u) sh->stage[wave][off++] = (uint16_t)(lane * 32u + __builtin_ctz(b));
-        if (lane == 0 && total) atomicSub(&sh->count[best], total);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
-        return total;
-    }
-    /* Which lane runs which slot.  A slot's period column is 4 * (slot % 64) of its 256-byte rows, so two lanes of
-     * one 32-lane LDS access group whose slots agree mod 32 hit the same bank on every period read and store.
-     * Slot id = word * 32 + bit, so its conflict-free lane is ((word & 1) << 5) | bit: every id goes there unless
-     * an earlier word of the same parity claimed that bit too; those few overflow into the free lanes.  (Packing
-     * the ids densely in claim order left 3.4 % of the CU cycles in bank conflicts, profiles/prof_pdf_r6_r03a.) */
-    const uint64_t mine = (uint64_t)got << ((lane & 1u) << 5);
-    uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32), ng = __builtin_popcount(got), no;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {                          /* inclusive OR-scan of mine, +-scan of ng */
-        const uint32_t ol = __shfl_up(lo, d, 64), oh = __shfl_up(hi, d, 64), on = __shfl_up(ng, d, 64);
-        if (lane >= (uint32_t)d) { lo |= ol; hi |= oh; ng += on; }
-    }
-    const uint32_t total = __builtin_amdgcn_readlane(ng, 63);
-    /* (readlane returns int: widen through uint32_t, or the low word's bit 31 would sign-extend into the high half) */
-    const uint64_t all = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 63) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane(lo, 63);
-    uint64_t excl = ((uint64_t)__shfl_up(hi, 1, 64) << 32) | __shfl_up(lo, 1, 64);
-    if (lane == 0) excl = 0;
-    const uint64_t over = mine & excl;                          /* natural lane already taken */
-    no = __builtin_popcountll(over);
-    uint32_t orank = no;
+    /* ids packed densely in claim order.  Measured and dropped (round 3): placing each slot id on lane id % 64 so that
+     * the lanes of one 32-lane LDS access group hit distinct period-column banks -- conflicts 3.4 -> 3.0 % of the CU
+     * cycles, but 3.50 -> 3.46 M cand/s for the extra scans */
+    const uint32_t ng = __builtin_popcount(got);
+    uint32_t off = ng;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(orank, d, 64);
-        if (lane >= (uint32_t)d) orank += o;
+        const uint32_t o = __shfl_up(off, d, 64);
+        if (lane >= (uint32_t)d) off += o;
     }
-    orank -= no;
-    sh->stage[wave][lane] = (uint16_t)0xffffu;                  /* in order with the writes below (one wave) */
-    for (uint64_t b = mine & ~excl; b; b &= b - 1u) {
-        const uint32_t pos = (uint32_t)__builtin_ctzll(b);
-        sh->stage[wave][pos] = (uint16_t)(lane * 32u + (pos & 31u));
-    }
-    if (over) {
-        uint64_t f = ~all;                                      /* free lanes; skip the ones lower lanes take */
-        for (uint32_t k = orank; k; k--) f &= f - 1u;
-        for (uint64_t b = over; b; b &= b - 1u) {
-            const uint32_t pos = (uint32_t)__builtin_ctzll(f);
-            f &= f - 1u;
-            sh->stage[wave][pos] = (uint16_t)(lane * 32u + ((uint32_t)__builtin_ctzll(b) & 31u));
-        }
-    }
+    const uint32_t total = __builtin_amdgcn_readlane(off, 63);
+    off -= ng;
+    for (uint32_t b = got; b; b &= b - 1u) sh->stage[wave][off++] = (uint16_t)(lane * 32u + __builtin_ctz(b));
     if (lane == 0 && total) atomicSub(&sh->count[best], total);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
-    const uint32_t st = sh->stage[wave][lane];
-    *slot = st == 0xffffu ? R6_IDLE : st;
+    *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
     return total;
 }
-
 #ifdef DPRF_R6_TIMING
 /* debug builds (-DDPRF_R6_TIMING): per-wave cycles in rounds vs waiting for queued slots */
 #define R6T_DECL unsigned long long t_work = 0, t_wait = 0, t_x = __builtin_readcyclecounter(), t_nb = 0, t_part = 0;

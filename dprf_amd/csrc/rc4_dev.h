@@ -122,11 +122,14 @@ DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
     uint32_t kb[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) kb[q] = k[q >> 2] >> (8 * (q & 3));    /* only the low byte is used */
-    uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s;
+    uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s, wn;
+    uint64_t c0, c1, c2, c3, h0;                       /* SGPR pairs of the prefetch variant (A/B headers) */
+#define RC4_KSA_OUTS                                                                                               \
+    "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st), "=&s"(m0s),   \
+        "=&v"(wn), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(h0)
     if constexpr (NK == 16) {
         asm volatile(RC4_KSA_ASM_16
-                     : "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st),
-                       "=&s"(m0s)
+                     : RC4_KSA_OUTS
                      : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1]), "v"(kb[2]), "v"(kb[3]), "v"(kb[4]),
                        "v"(kb[(5) % NK]), "v"(kb[(6) % NK]), "v"(kb[(7) % NK]), "v"(kb[(8) % NK]), "v"(kb[(9) % NK]),
                        "v"(kb[(10) % NK]), "v"(kb[(11) % NK]), "v"(kb[(12) % NK]), "v"(kb[(13) % NK]),
@@ -134,12 +137,12 @@ DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
                      : "vcc", "memory");
     } else {
         asm volatile(RC4_KSA_ASM_5
-                     : "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st),
-                       "=&s"(m0s)
+                     : RC4_KSA_OUTS
                      : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1 % NK]), "v"(kb[2 % NK]), "v"(kb[3 % NK]),
                        "v"(kb[4 % NK])
                      : "vcc", "memory");
     }
+#undef RC4_KSA_OUTS
 }
 
 /* R2 (one KSA per candidate) runs the same rc4_ksa; its round-1 one-step-ahead KSA (S[j] and S[i+1] read

@@ -16,8 +16,8 @@ HDR = os.path.join(HERE, "..", "dprf_amd", "csrc", "rc4_ksa_asm.h")
 LANES = 64
 
 
-def program(nk):
-    text = open(HDR).read()
+def program(nk, text=None):
+    text = text if text is not None else open(HDR).read()
     m = re.search(r"#define RC4_KSA_ASM_%d \\\n(.*?)\n    \"\"" % nk, text, re.S)
     assert m, nk
     return [ln.strip()[1:-len('\\n\\t" \\')] for ln in m.group(1).splitlines()]
@@ -43,9 +43,10 @@ def emulate(prog, keys, nk, sbase=0):
         w = np.array([int.from_bytes(bytes(k[(q & ~3):(q & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
                      dtype=np.uint64)
         kb.append(w >> np.uint64(8 * (q & 3)))            # garbage above byte 0, as the kernel passes them
-    vin = {"%10": sbase + 4 * lane, "%11": sbase}
+    vin = {"%16": sbase + 4 * lane, "%17": sbase}
     for q in range(nk):
-        vin["%%%d" % (12 + q)] = kb[q]
+        vin["%%%d" % (18 + q)] = kb[q]
+    masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
     vcc = np.zeros(LANES, dtype=bool)
     M32 = np.uint64(0xffffffff)
 
@@ -76,6 +77,11 @@ def emulate(prog, keys, nk, sbase=0):
         last = a[-1].split() if a else []
         if op == "s_mov_b32":
             sregs[a[0]] = s(a[1])
+        elif op == "s_mov_b64":
+            assert a[0] == "vcc"
+            vcc = masks[a[1]].copy()
+        elif op == "s_nop":
+            pass
         elif op == "s_movk_i32":
             sregs[a[0]] = int(a[1], 0)
         elif op == "s_waitcnt":
@@ -99,8 +105,12 @@ def emulate(prog, keys, nk, sbase=0):
             shifted = (src >> np.uint64(int(a[1]))) & np.uint64(0xff)
             regs[a[0]] = (regs[a[0]] & ~np.uint64(0xff00) & M32) | (shifted << np.uint64(8))
         elif op == "v_cmp_eq_u32_sdwa":
-            assert a[0] == "vcc" and "src0_sel:BYTE_0" in ln
-            vcc = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(a[2].split()[0]))
+            assert "src0_sel:BYTE_0" in ln
+            r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(a[2].split()[0]))
+            if a[0] == "vcc":
+                vcc = r
+            else:
+                masks[a[0]] = r
         elif op == "ds_read_u8":
             regs[a[0]] = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
         elif op == "ds_write_b8":
@@ -123,9 +133,11 @@ def emulate(prog, keys, nk, sbase=0):
             sh0, m0_ = sel[re.search(r"src0_sel:(\w+)", ln).group(1)]
             sh1, m1_ = sel[re.search(r"src1_sel:(\w+)", ln).group(1)]
             r = np.where(vcc, (s1 >> np.uint64(sh1)) & np.uint64(m1_), (s0 >> np.uint64(sh0)) & np.uint64(m0_))
-            if "dst_sel:BYTE_1" in ln:
+            dsel = re.search(r"dst_sel:(\w+)", ln).group(1)
+            if dsel in ("BYTE_0", "BYTE_1"):
                 assert "UNUSED_PRESERVE" in ln
-                regs[a[0]] = (regs[a[0]] & ~np.uint64(0xff00) & M32) | ((r & np.uint64(0xff)) << np.uint64(8))
+                sh = np.uint64(0 if dsel == "BYTE_0" else 8)
+                regs[a[0]] = (regs[a[0]] & ~(np.uint64(0xff) << sh) & M32) | ((r & np.uint64(0xff)) << sh)
             else:
                 assert "dst_sel:DWORD" in ln
                 regs[a[0]] = r
@@ -151,6 +163,22 @@ def test_generated_ksa_equals_rc4(nk):
         got = emulate(prog, keys, nk)
         for l_ in range(LANES):
             assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
+
+
+@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch"])
+def test_schedule_variants_equal_rc4(flag):
+    """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
+    group's S[j] stores and repairs it) compute the same key schedule."""
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    text = subprocess.run([sys.executable, gen, flag], capture_output=True, text=True, check=True).stdout
+    for nk in (5, 16):
+        rng = random.Random(nk + 100)
+        keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
+        keys[0], keys[1], keys[2] = [0] * 16, [1] * 16, [2] * 16
+        got = emulate(program(nk, text), keys, nk)
+        assert all(got[l_] == ref_ksa(keys[l_], nk) for l_ in range(LANES)), (flag, nk)
 
 
 def test_header_is_what_the_generator_writes():

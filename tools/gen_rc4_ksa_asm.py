@@ -32,6 +32,8 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
        tools/gen_rc4_ksa_asm.py --early-read > <variant header>   (A/B: each S[j] read one instruction earlier)
        tools/gen_rc4_ksa_asm.py --late-merge > <variant header>   (A/B: group q-1's S[i] merge + store issued
                                                                     inside group q, between a0 and the S[j] read)
+       tools/gen_rc4_ksa_asm.py --prefetch > <variant header>     (A/B: the next pair read at the start of each
+                                                                    group and repaired for its S[j] stores)
 """
 
 KEYLENS = (5, 16)   # R2 / R3-R4 with 40-bit keys use 5 bytes, R3/R4 128-bit keys 16 (EVP_rc4 reads 16)
@@ -42,22 +44,18 @@ def pos(i):
     return ((i >> 2) << 8) + (i & 3)
 
 
-def ksa(nk, early_read=False, late_merge=False):
-    # operands: %0 j (in/out), %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR),
-    #           %10 lanebase, %11 sbase (SGPR, the area's LDS address for ds_write_addtid), %12.. key bytes
-    J, W, X0, X1, V1, A0, A1, M, ST, M0S, LB, SB = ("%%%d" % k for k in range(12))
-    KB = ["%%%d" % (12 + k) for k in range(nk)]
+def ksa(nk, early_read=False, late_merge=False, prefetch=False):
+    # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn,
+    #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
+    #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18.. key bytes
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB = ("%%%d" % k for k in range(18))
+    KB = ["%%%d" % (18 + k) for k in range(nk)]
+    if prefetch:
+        return ksa_prefetch(nk, J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, KB)
     out = []
     e = out.append
     # identity: dword w of lane l at area + 256 w + 4 l = M0 + offset + 4 * lane
-    e("s_mov_b32 %s, m0" % M0S)
-    e("s_mov_b32 m0, %s" % SB)
-    e("v_mov_b32 %s, 0x3020100" % M)
-    for w in range(64):
-        e("ds_write_addtid_b32 %s offset:%d" % (M, 256 * w))
-        if w < 63:
-            e("v_add_u32 %s, 0x4040404, %s" % (M, M))
-    e("s_mov_b32 m0, %s" % M0S)
+    identity(e, M, M0S, SB)
     e("v_mov_b32 %s, 0" % J)
     e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
     def merge(q):
@@ -119,15 +117,95 @@ def ksa(nk, early_read=False, late_merge=False):
     return out
 
 
+def identity(e, M, M0S, SB):
+    e("s_mov_b32 %s, m0" % M0S)
+    e("s_mov_b32 m0, %s" % SB)
+    e("v_mov_b32 %s, 0x3020100" % M)
+    for w in range(64):
+        e("ds_write_addtid_b32 %s offset:%d" % (M, 256 * w))
+        if w < 63:
+            e("v_add_u32 %s, 0x4040404, %s" % (M, M))
+    e("s_mov_b32 m0, %s" % M0S)
+
+
+def ksa_prefetch(nk, J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, KB):
+    """The next group's pair is read at the START of a group -- its LDS latency overlaps the group instead of
+    sitting on the j chain between groups -- and repaired afterwards for this group's two S[j] stores (j0 stored
+    W.byte0, j1 stored v1; a later store wins).  W and Wn swap roles every group (no copy)."""
+    out = []
+    e = out.append
+    identity(e, M, M0S, SB)
+    e("v_mov_b32 %s, 0" % J)
+    e("v_mov_b32 %s, 0x100" % W)
+    regs = [W, WN]
+    for q in range(128):
+        i0, i1, p2, p3 = 2 * q, 2 * q + 1, 2 * q + 2, 2 * q + 3
+        w, wn = regs[q & 1], regs[(q + 1) & 1]
+        last = q == 127
+        if not last:
+            e("ds_read_u16 %s, %s offset:%d" % (wn, LB, pos(p2)))
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, w, KB[i0 % nk]))
+        e("s_movk_i32 %s, %d" % (ST, i1))
+        e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A0, J))
+        e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        e("ds_read_u8 %s, %s" % (X0, A0))
+        e("ds_write_b8 %s, %s" % (A0, w))
+        if not last:
+            e("s_movk_i32 %s, %d" % (ST, p2))
+            e("v_cmp_eq_u32_sdwa %s, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (C0, J, ST))
+            e("s_movk_i32 %s, %d" % (ST, p3))
+            e("v_cmp_eq_u32_sdwa %s, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (C1, J, ST))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
+          % (V1, w, w))
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
+        e("s_movk_i32 %s, %d" % (ST, i0))
+        e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A1, J))
+        e("v_cmp_eq_u32_sdwa %s, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (H0, J, ST))
+        e("ds_read_u8 %s, %s" % (X1, A1))
+        e("ds_write_b8 %s, %s" % (A1, V1))
+        if not last:
+            e("s_movk_i32 %s, %d" % (ST, p2))
+            e("v_cmp_eq_u32_sdwa %s, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (C2, J, ST))
+            e("s_movk_i32 %s, %d" % (ST, p3))
+            e("v_cmp_eq_u32_sdwa %s, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (C3, J, ST))
+        # x0, x1 and the prefetched pair have landed (only the S[j1] store may still be in flight)
+        e("s_waitcnt lgkmcnt(1)")
+        e("s_mov_b64 vcc, %s" % H0)
+        e("s_nop 1")
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+          % (M, X1, X0))
+        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(i0)))
+        if not last:
+            # S[p2] = byte 0 of wn, S[p3] = byte 1: j0's store (W.byte0) first, then j1's (v1)
+            for cond, src, sel in ((C0, w, "BYTE_0"), (C2, V1, "BYTE_0")):
+                e("s_mov_b64 vcc, %s" % cond)
+                e("s_nop 1")
+                e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 "
+                  "src1_sel:%s" % (wn, wn, src, sel))
+            for cond, src, sel in ((C1, w, "BYTE_0"), (C3, V1, "BYTE_0")):
+                e("s_mov_b64 vcc, %s" % cond)
+                e("s_nop 1")
+                e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 "
+                  "src1_sel:%s" % (wn, wn, src, sel))
+    e("s_waitcnt lgkmcnt(0)")
+    return out
+
+
 def main():
     import sys
     early = "--early-read" in sys.argv      # A/B variants (tools/build_variant.sh with RC4_KSA_ASM_HEADER)
     late = "--late-merge" in sys.argv
+    pre = "--prefetch" in sys.argv
     print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
     print("#ifndef DPRF_RC4_KSA_ASM_H")
     print("#define DPRF_RC4_KSA_ASM_H")
     for nk in KEYLENS:
-        lines = ksa(nk, early, late)
+        lines = ksa(nk, early, late, pre)
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
