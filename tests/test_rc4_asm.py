@@ -106,7 +106,12 @@ def emulate(prog, keys, nk, sbase=0):
             regs[a[0]] = (regs[a[0]] & ~np.uint64(0xff00) & M32) | (shifted << np.uint64(8))
         elif op == "v_cmp_eq_u32_sdwa":
             assert "src0_sel:BYTE_0" in ln
-            r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(a[2].split()[0]))
+            src1 = a[2].split()[0]
+            if src1.startswith("%") and src1 not in sregs and src1 not in vin:      # a VGPR, byte-selected
+                sh1 = {"BYTE_0": 0, "BYTE_1": 8}[re.search(r"src1_sel:(\w+)", ln).group(1)]
+                r = (v(a[1]) & np.uint64(0xff)) == ((v(src1) >> np.uint64(sh1)) & np.uint64(0xff))
+            else:
+                r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(src1))
             if a[0] == "vcc":
                 vcc = r
             else:
@@ -165,7 +170,7 @@ def test_generated_ksa_equals_rc4(nk):
             assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
 
 
-@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch"])
+@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--vgpr-consts"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""

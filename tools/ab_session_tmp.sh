@@ -1,13 +1,7 @@
-mkdir -p gpurun_out
-ab() { W=$1; shift; for V in "$@"; do
-  if [ "$V" = "base" ]; then L=$PWD/dprf_amd/libdprf.so; else L=$PWD/build/ab/libdprf_$V.so; fi
-  for rep in 1 2; do DPRF_LIB=$L timeout -k 5 150 python bench.py --workload $W --no-side --cpu-seconds 0 --steps 3 | python -c "import json,sys; d=json.load(sys.stdin); print('$W $V', d['value'], d['roofline']['frac'], d['roofline']['kernel_avg_ms'])"; done
-done; }
-DPRF_LIB=$PWD/build/ab/libdprf_r24_pre.so timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py tests/test_full_size.py tests/test_docs.py -m gpu -x -q --timeout 120 --timeout-method thread -k "pdf or r24 or r34 or r2 or R4 or R3 or R2" > gpurun_out/gputests_pre.log 2>&1
-echo "pre tests rc=$? $(tail -1 gpurun_out/gputests_pre.log)"
-ab pdf_r34 base r24_pre
-ab pdf_r2 base r24_pre
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_r03e.log 2>&1
-echo "tests rc=$? $(tail -1 gpurun_out/gputests_r03e.log)"
-ab pdf_r6 base
-echo done
+set -e
+bash tools/gpu_session.sh r03b
+echo "== n2 library-mode rehearsal $(date +%T)"
+DPRF_BENCH_SAME_DEVICE=1 timeout -k 10 200 python bench.py --gpus 2 --no-side --cpu-seconds 0 --no-cluster > gpurun_out/bench_lanes2_r03b.json 2> gpurun_out/bench_lanes2_r03b.err
+python -c "import json; d=json.load(open('gpurun_out/bench_lanes2_r03b.json')); print(d['value'], d.get('device_balance',{}).get('last_over_mean'))"
+DPRF_BENCH_SAME_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --workload pdf_r6 --no-side --cpu-seconds 0 --no-cluster --steps 2 > gpurun_out/bench_lanes2_r6_r03b.json 2>> gpurun_out/bench_lanes2_r03b.err
+python -c "import json; d=json.load(open('gpurun_out/bench_lanes2_r6_r03b.json')); print(d['value'], d.get('device_balance',{}).get('last_over_mean'))"

@@ -34,6 +34,8 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     inside group q, between a0 and the S[j] read)
        tools/gen_rc4_ksa_asm.py --prefetch > <variant header>     (A/B: the next pair read at the start of each
                                                                     group and repaired for its S[j] stores)
+       tools/gen_rc4_ksa_asm.py --vgpr-consts > <variant header>  (A/B: compare constants (i0, i1) from one VGPR
+                                                                    bumped per group instead of two SALU moves)
 """
 
 KEYLENS = (5, 16)   # R2 / R3-R4 with 40-bit keys use 5 bytes, R3/R4 128-bit keys 16 (EVP_rc4 reads 16)
@@ -44,7 +46,7 @@ def pos(i):
     return ((i >> 2) << 8) + (i & 3)
 
 
-def ksa(nk, early_read=False, late_merge=False, prefetch=False):
+def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18.. key bytes
@@ -58,6 +60,9 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False):
     identity(e, M, M0S, SB)
     e("v_mov_b32 %s, 0" % J)
     e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
+    IC = WN                              # vconst: (i0, i1) of the group in bytes 0, 1 of a VGPR
+    if vconst:
+        e("v_mov_b32 %s, 0x100" % IC)
     def merge(q):
         """the deferred S[i0], S[i1] of group q as one u16 (VCC = hit0 of group q)"""
         e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
@@ -70,7 +75,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False):
         if q > 0:
             e("s_waitcnt lgkmcnt(%d)" % (0 if late_merge else 1))
         e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
-        e("s_movk_i32 %s, %d" % (ST, i1))
+        if not vconst:
+            e("s_movk_i32 %s, %d" % (ST, i1))
         e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
           % (A0, J))
@@ -81,6 +87,10 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False):
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_write_b8 %s, %s" % (A0, W))
             e("s_movk_i32 %s, %d" % (ST, i0))
+        elif vconst:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_1" % (J, IC))
+            e("ds_read_u8 %s, %s" % (X0, A0))
+            e("ds_write_b8 %s, %s" % (A0, W))
         else:
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_read_u8 %s, %s" % (X0, A0))
@@ -88,7 +98,7 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False):
         e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
           % (V1, W, W))
         e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
-        if not early_read:
+        if not early_read and not vconst:
             e("s_movk_i32 %s, %d" % (ST, i0))
         e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
@@ -96,10 +106,15 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False):
         if early_read:
             e("ds_read_u8 %s, %s" % (X1, A1))
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        elif vconst:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_0" % (J, IC))
+            e("ds_read_u8 %s, %s" % (X1, A1))
         else:
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_read_u8 %s, %s" % (X1, A1))
         e("ds_write_b8 %s, %s" % (A1, V1))
+        if vconst and q < 127:
+            e("v_add_u32 %s, 0x202, %s" % (IC, IC))
         if late_merge:
             if q < 127:
                 e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
@@ -201,11 +216,12 @@ def main():
     early = "--early-read" in sys.argv      # A/B variants (tools/build_variant.sh with RC4_KSA_ASM_HEADER)
     late = "--late-merge" in sys.argv
     pre = "--prefetch" in sys.argv
+    vconst = "--vgpr-consts" in sys.argv
     print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
     print("#ifndef DPRF_RC4_KSA_ASM_H")
     print("#define DPRF_RC4_KSA_ASM_H")
     for nk in KEYLENS:
-        lines = ksa(nk, early, late, pre)
+        lines = ksa(nk, early, late, pre, vconst)
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
