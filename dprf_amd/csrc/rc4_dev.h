@@ -124,23 +124,29 @@ DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
     for (int q = 0; q < NK; q++) kb[q] = k[q >> 2] >> (8 * (q & 3));    /* only the low byte is used */
     uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s, wn;
     uint64_t c0, c1, c2, c3, h0;                       /* SGPR pairs of the prefetch variant (A/B headers) */
+    /* the identity by ds_write_b128: lane l writes row 4t + l/16, bytes 16 (l%16) .. +16, for t = 0..15, first
+     * value 0x03020100 + 0x04040404 (l/16) in every dword, +0x10101010 per t (gen_rc4_ksa_asm.py identity_b128) */
+    const uint32_t l4 = lanebase - sbase;                /* 4 * lane */
+    const uint32_t ia = sbase + ((l4 >> 6) << 8) + ((l4 & 60u) << 2);
+    const uint32_t d0 = 0x03020100u + 0x04040404u * (l4 >> 6);
+    const uint64_t c16 = 0x1010101010101010ull;
 #define RC4_KSA_OUTS                                                                                               \
     "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st), "=&s"(m0s),   \
         "=&v"(wn), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(h0)
     if constexpr (NK == 16) {
         asm volatile(RC4_KSA_ASM_16
                      : RC4_KSA_OUTS
-                     : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1]), "v"(kb[2]), "v"(kb[3]), "v"(kb[4]),
-                       "v"(kb[(5) % NK]), "v"(kb[(6) % NK]), "v"(kb[(7) % NK]), "v"(kb[(8) % NK]), "v"(kb[(9) % NK]),
-                       "v"(kb[(10) % NK]), "v"(kb[(11) % NK]), "v"(kb[(12) % NK]), "v"(kb[(13) % NK]),
-                       "v"(kb[(14) % NK]), "v"(kb[(15) % NK])
-                     : "vcc", "memory");
+                     : "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0), "v"(kb[0]), "v"(kb[1]), "v"(kb[2]),
+                       "v"(kb[3]), "v"(kb[4]), "v"(kb[(5) % NK]), "v"(kb[(6) % NK]), "v"(kb[(7) % NK]),
+                       "v"(kb[(8) % NK]), "v"(kb[(9) % NK]), "v"(kb[(10) % NK]), "v"(kb[(11) % NK]),
+                       "v"(kb[(12) % NK]), "v"(kb[(13) % NK]), "v"(kb[(14) % NK]), "v"(kb[(15) % NK])
+                     : "vcc", "memory", "v60", "v61", "v62", "v63");
     } else {
         asm volatile(RC4_KSA_ASM_5
                      : RC4_KSA_OUTS
-                     : "v"(lanebase), "s"(sbase), "v"(kb[0]), "v"(kb[1 % NK]), "v"(kb[2 % NK]), "v"(kb[3 % NK]),
-                       "v"(kb[4 % NK])
-                     : "vcc", "memory");
+                     : "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0), "v"(kb[0]), "v"(kb[1 % NK]),
+                       "v"(kb[2 % NK]), "v"(kb[3 % NK]), "v"(kb[4 % NK])
+                     : "vcc", "memory", "v60", "v61", "v62", "v63");
     }
 #undef RC4_KSA_OUTS
 }

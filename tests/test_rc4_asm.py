@@ -43,9 +43,12 @@ def emulate(prog, keys, nk, sbase=0):
         w = np.array([int.from_bytes(bytes(k[(q & ~3):(q & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
                      dtype=np.uint64)
         kb.append(w >> np.uint64(8 * (q & 3)))            # garbage above byte 0, as the kernel passes them
-    vin = {"%16": sbase + 4 * lane, "%17": sbase}
+    l4 = 4 * lane
+    vin = {"%16": sbase + l4, "%17": sbase,
+           "%18": sbase + ((l4 >> np.uint64(6)) << np.uint64(8)) + ((l4 & np.uint64(60)) << np.uint64(2)),
+           "%19": 0x1010101010101010, "%20": np.uint64(0x03020100) + np.uint64(0x04040404) * (l4 >> np.uint64(6))}
     for q in range(nk):
-        vin["%%%d" % (18 + q)] = kb[q]
+        vin["%%%d" % (21 + q)] = kb[q]
     masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
     vcc = np.zeros(LANES, dtype=bool)
     M32 = np.uint64(0xffffffff)
@@ -120,6 +123,21 @@ def emulate(prog, keys, nk, sbase=0):
             regs[a[0]] = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
         elif op == "ds_write_b8":
             lds[v(a[0]).astype(np.int64)] = (v(a[1]) & np.uint64(0xff)).astype(np.uint8)
+        elif op == "ds_write_b128":
+            assert a[1].split()[0] == "v[60:63]"
+            o = off(a[1].split()[1]) if len(a[1].split()) > 1 else 0
+            ad = (v(a[0]) + np.uint64(o)).astype(np.int64)
+            for k in range(4):
+                val = regs["v%d" % (60 + k)]
+                for b in range(4):
+                    lds[ad + 4 * k + b] = ((val >> np.uint64(8 * b)) & np.uint64(0xff)).astype(np.uint8)
+        elif op == "v_lshl_add_u64":
+            m = re.match(r"v\[(\d+):(\d+)\]", a[0])
+            lo_, hi_ = "v%s" % m.group(1), "v%s" % m.group(2)
+            assert a[1] == a[0] and a[2] == "0"
+            x = regs[lo_] | (regs[hi_] << np.uint64(32))
+            x = x + np.uint64(s(a[3]))
+            regs[lo_], regs[hi_] = x & M32, x >> np.uint64(32)
         elif op == "ds_read_u16":
             base, o = a[1].split()[0], off(a[1].split()[1])
             ad = (v(base) + np.uint64(o)).astype(np.int64)
@@ -170,7 +188,7 @@ def test_generated_ksa_equals_rc4(nk):
             assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
 
 
-@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--vgpr-consts"])
+@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""

@@ -4,15 +4,21 @@ block per key length (pdf_password_verifier.c:157-176 via EVP_rc4; RC4 itself: S
 j += S[i] + K[i % n]; swap(S[i], S[j])).
 
 Why asm: the compiled C++ schedule (rc4_dev.h rc4_ksa) issues 16-17 VALU instructions per group of two steps
-(~31 issue slots: byte extracts, compare + select pairs, a u16 merge in two steps); the same dataflow fits in 11,
-~21 slots, with the byte selects folded into SDWA operands -- and only asm keeps LLVM from re-materialising or
-re-ordering them.  The schedule is rc4_ksa's group-deferred one (rc4_dev.h): per group q (i0 = 2q, i1 = 2q + 1)
+(~31 issue slots: byte extracts, compare + select pairs, a u16 merge in two steps); the same dataflow fits in 12,
+with the byte selects folded into SDWA operands -- and only asm keeps LLVM from re-materialising or re-ordering
+them.  What bounds this loop on gfx950 is the length of each wave's instruction stream (LdsUtil 0.5, VALU not
+saturated, 9 waves per CU): every variant that added instructions lost, every one that removed some won, so the
+schedule minimises instructions per group (20; 19 while the compare constants are inline), SALU included --
+except that LDS time counts too: 16 ds_write_b128 for the identity instead of 64 ds_write_addtid_b32 (48 instead
+of 131 instructions per KSA) lost 3 %.  The schedule is rc4_ksa's group-deferred one
+(rc4_dev.h): per group q (i0 = 2q, i1 = 2q + 1)
 
     wait for W = S[i0] | S[i1] << 8            (read at the end of group q - 1; lgkmcnt(1): the u16 store
                                                  issued after it may stay in flight -- LDS completes in order)
     j += W + K[i0]                              (only j's low byte is ever used: W's byte 1 above it is harmless)
     a0 = (j & 3) | lanebase; a0.byte1 = j.byte0 >> 2            -> address of S[j] in the [i/4][lane][i%4] layout
-    hit1 = (j.byte0 == i1)
+    hit1 = (j.byte0 == i1)                      (i1 an inline constant while <= 64, else byte 1 of a VGPR (i0, i1)
+                                                 bumped by 0x0202 once per group: no SALU in the loop)
     x0 = S[j]; S[j] = W.byte0
     v1 = hit1 ? W.byte0 : W.byte1               (one SDWA cndmask: the current S[i1])
     j += v1 + K[i1];  a1 likewise;  hit0 = (j.byte0 == i0)
@@ -22,11 +28,11 @@ re-ordering them.  The schedule is rc4_ksa's group-deferred one (rc4_dev.h): per
     m = hit0 ? v1 : x0;  m.byte1 = hit0 ? x0 : x1                -> S[i0], S[i1] as one u16
     store m at S[i0]
 
-Hazards: every VCC consumer (v_cndmask) is at least two instructions after the v_cmp that writes VCC (the LDS
-instructions in between count as wait states).  The block writes the identity itself (ds_write_addtid_b32 through
-M0, restored at the end) and ends with lgkmcnt(0), so the compiler never sees an LDS operation of this block in
-flight.  Requirements (checked by the caller): the S-box area starts at an LDS address whose low 16 bits are zero
-(the SDWA byte-1 insert overwrites bits 8-15 of lanebase) and lanebase = area + 4 * lane.
+The identity is written by 64 ds_write_addtid_b32 (identity; identity_b128 measured slower).  Hazards: every VCC consumer (v_cndmask) is at
+least two instructions after the v_cmp that writes VCC (the LDS instructions in between count as wait states).
+The block ends with lgkmcnt(0), so the compiler never sees an LDS operation of this block in flight.
+Requirements (checked by the caller): the S-box area starts at an LDS address whose low 16 bits are zero (the
+SDWA byte-1 insert overwrites bits 8-15 of lanebase) and lanebase = area + 4 * lane.
 
 Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
        tools/gen_rc4_ksa_asm.py --early-read > <variant header>   (A/B: each S[j] read one instruction earlier)
@@ -34,8 +40,11 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     inside group q, between a0 and the S[j] read)
        tools/gen_rc4_ksa_asm.py --prefetch > <variant header>     (A/B: the next pair read at the start of each
                                                                     group and repaired for its S[j] stores)
-       tools/gen_rc4_ksa_asm.py --vgpr-consts > <variant header>  (A/B: compare constants (i0, i1) from one VGPR
-                                                                    bumped per group instead of two SALU moves)
+       tools/gen_rc4_ksa_asm.py --salu-consts > <variant header>  (A/B, round-3 first version: compare constants
+                                                                    through two s_movk per group)
+       tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
+                                                                    64-bit adds: 612 -> 595 M, the b128 stores cost
+                                                                    more LDS time than the instructions they save)
 """
 
 KEYLENS = (5, 16)   # R2 / R3-R4 with 40-bit keys use 5 bytes, R3/R4 128-bit keys 16 (EVP_rc4 reads 16)
@@ -46,23 +55,30 @@ def pos(i):
     return ((i >> 2) << 8) + (i & 3)
 
 
-def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False):
-    # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn,
+def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False):
+    # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
-    #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18.. key bytes
-    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB = ("%%%d" % k for k in range(18))
-    KB = ["%%%d" % (18 + k) for k in range(nk)]
+    #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
+    #           (VGPR), %19 0x1010101010101010 (SGPR pair), %20 first identity dword of the lane, %21.. key bytes;
+    #           the b128 identity's data quad is the clobbered v[60:63] (a register tuple operand cannot be split)
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, IA, C16, D0 = (
+        "%%%d" % k for k in range(21))
+    KB = ["%%%d" % (21 + k) for k in range(nk)]
     if prefetch:
         return ksa_prefetch(nk, J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, KB)
     out = []
     e = out.append
-    # identity: dword w of lane l at area + 256 w + 4 l = M0 + offset + 4 * lane
-    identity(e, M, M0S, SB)
+    # identity: dword w of lane l at area + 256 w + 4 l
+    if b128:
+        identity_b128(e, IA, C16, D0)
+    else:
+        identity(e, M, M0S, SB)
     e("v_mov_b32 %s, 0" % J)
     e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
-    IC = WN                              # vconst: (i0, i1) of the group in bytes 0, 1 of a VGPR
+    IC = WN                              # vconst: (i0, i1) of the group in bytes 0, 1 of a VGPR, from the first
+    FIRST_IC = 32 if vconst else 0       # group whose i1 is past the inline constants (0..64)
     if vconst:
-        e("v_mov_b32 %s, 0x100" % IC)
+        e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
     def merge(q):
         """the deferred S[i0], S[i1] of group q as one u16 (VCC = hit0 of group q)"""
         e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
@@ -88,7 +104,10 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False):
             e("ds_write_b8 %s, %s" % (A0, W))
             e("s_movk_i32 %s, %d" % (ST, i0))
         elif vconst:
-            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_1" % (J, IC))
+            if q < FIRST_IC:
+                e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i1))
+            else:
+                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_1" % (J, IC))
             e("ds_read_u8 %s, %s" % (X0, A0))
             e("ds_write_b8 %s, %s" % (A0, W))
         else:
@@ -107,13 +126,16 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False):
             e("ds_read_u8 %s, %s" % (X1, A1))
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
         elif vconst:
-            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_0" % (J, IC))
+            if q < FIRST_IC:
+                e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i0))
+            else:
+                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_0" % (J, IC))
             e("ds_read_u8 %s, %s" % (X1, A1))
         else:
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_read_u8 %s, %s" % (X1, A1))
         e("ds_write_b8 %s, %s" % (A1, V1))
-        if vconst and q < 127:
+        if vconst and FIRST_IC <= q < 127:
             e("v_add_u32 %s, 0x202, %s" % (IC, IC))
         if late_merge:
             if q < 127:
@@ -141,6 +163,25 @@ def identity(e, M, M0S, SB):
         if w < 63:
             e("v_add_u32 %s, 0x4040404, %s" % (M, M))
     e("s_mov_b32 m0, %s" % M0S)
+
+
+IDQ = ("v[60:63]", "v[60:61]", "v[62:63]", ("v60", "v61", "v62", "v63"))
+
+
+def identity_b128(e, IA, C16, D0):
+    """The identity as 16 ds_write_b128 instead of 64 ds_write_addtid_b32 + 63 v_add: lane l writes 16 bytes of row
+    4t + l/16 (lanes 4(l%16) .. 4(l%16)+3 of it, which all hold the same identity dword) at IA = area + 256 (l/16)
+    + 16 (l%16) + 1024 t; its data quad starts at 0x03020100 + 0x04040404 (l/16) (D0) in every dword and moves four
+    rows on (+0x10101010 per dword) with two 64-bit adds.  LDS cycles: 16 x ~13 instead of 64 x 2 (the LDS pipe has
+    room, LdsUtil 0.5); instructions: 50 instead of 131 per KSA."""
+    quad, lo, hi, regs = IDQ
+    for r in regs:
+        e("v_mov_b32 %s, %s" % (r, D0))
+    for t in range(16):
+        e("ds_write_b128 %s, %s offset:%d" % (IA, quad, 1024 * t))
+        if t < 15:
+            e("v_lshl_add_u64 %s, %s, 0, %s" % (lo, lo, C16))
+            e("v_lshl_add_u64 %s, %s, 0, %s" % (hi, hi, C16))
 
 
 def ksa_prefetch(nk, J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, KB):
@@ -216,12 +257,13 @@ def main():
     early = "--early-read" in sys.argv      # A/B variants (tools/build_variant.sh with RC4_KSA_ASM_HEADER)
     late = "--late-merge" in sys.argv
     pre = "--prefetch" in sys.argv
-    vconst = "--vgpr-consts" in sys.argv
+    vconst = "--salu-consts" not in sys.argv
+    b128 = "--b128-identity" in sys.argv
     print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
     print("#ifndef DPRF_RC4_KSA_ASM_H")
     print("#define DPRF_RC4_KSA_ASM_H")
     for nk in KEYLENS:
-        lines = ksa(nk, early, late, pre, vconst)
+        lines = ksa(nk, early, late, pre, vconst and not early, b128)
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
