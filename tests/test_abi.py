@@ -53,3 +53,19 @@ def test_product_does_not_import_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 src = open(os.path.join(root, f), errors="replace").read()
                 assert "pyoracle" not in src and "liboracle" not in src and "oracle.h" not in src, f
+
+
+def test_makefile_tracks_every_local_header():
+    """Every header a kernel or host source includes is a make dependency and part of the build fingerprint
+    (HDRS): round 3 once shipped a stale object because the generated rc4_ksa_asm.h was missing there, so the
+    library -- and its dprf_build_id() -- did not change when the header did."""
+    import re
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dprf_amd", "csrc")
+    mk = open(os.path.join(csrc, "Makefile")).read()
+    hdrs = set(re.search(r"^HDRS\s*:=\s*(.*)$", mk, re.M).group(1).split())
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            for inc in re.findall(r'^#include "([^"]+)"', open(os.path.join(csrc, f)).read(), re.M):
+                if inc == "build_id.h":
+                    continue                      # generated into OBJDIR by the Makefile itself
+                assert inc in hdrs, (f, inc)
