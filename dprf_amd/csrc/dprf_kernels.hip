@@ -732,10 +732,23 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
          * keystream and the reference's complete 16-byte compare (:184-189) */
         for (uint32_t full = 0; full < 2u; full++) {
             uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
+            /* the asm KSA's key registers, made once per candidate; pass x's key (key ^ x) by XORing x ^ (x - 1)
+             * into their byte 0 (16 v_xor per pass, the same count as forming kx and extracting its bytes) */
+            uint32_t kb[rc4_nkr<NK>::v];
+            rc4_kb_init<NK>(h, kb);
             for (uint32_t x = 0; x < 20u; x++) {
-                const uint32_t xx = x * 0x01010101u;
-                uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
-                r24_ksa<NK>(Sw, sbase, lane, kx);
+                if (R24_KSA_ASM) {
+                    const uint32_t dx = x ^ (x - 1u);
+                    if (x) {
+#pragma unroll
+                        for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+                    }
+                    rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
+                } else {
+                    const uint32_t xx = x * 0x01010101u;
+                    uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
+                    rc4_ksa<NK>(Sw, lane << 2, kx);
+                }
                 if (full) rc4_prga<16>(Sw, lane << 2, d);
                 else rc4_prga<2>(Sw, lane << 2, d);
             }

@@ -43,6 +43,18 @@
  * R6_TE_USED <= 128 (fewer copies) bytes 128..255 of each row hold the periods of 32-slot groups
  * (slot_lds). */
 #define R6_TE_ROW_BYTES 256
+/* R6_SPLIT (default, round 3): four tables x 16 copies, lane groups A (lanes with bit 4 clear) and B read different
+ * tables in every lookup, so the 32 lanes of a ds_read_b32 half meet 32 banks, and no rotates are left (below,
+ * aes128_encrypt_split). */
+#ifndef R6_SPLIT
+#define R6_SPLIT 0
+#endif
+#if R6_SPLIT
+#undef R6_TABLES
+#undef R6_TE_COPIES
+#define R6_TABLES 4
+#define R6_TE_COPIES 16
+#endif
 #ifndef R6_TABLES
 #define R6_TABLES 2
 #endif
@@ -77,6 +89,9 @@ struct r6_lds {
     uint32_t pat;              /* LDS byte address of the slot's group: rows of 256 bytes */
     uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
     uint32_t lanec;            /* 4 * (thread lane % R6_TE_COPIES): this thread's table copy */
+#if R6_SPLIT
+    uint32_t base;             /* byte t: row offset of the copy of the table lookup t reads (A: T_t, B: T_t+1) */
+#endif
 };
 
 /* Te0[byte k of v] */
@@ -170,6 +185,136 @@ DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0,
     out[3] = (((teb<3>(S, s3) << 8) & 0xff000000u) | (teb<2>(S, s0) & 0x00ff0000u) |
               ((teb<1>(S, s1) >> 8) & 0x0000ff00u) | ((teb<0>(S, s2) >> 16) & 0xffu)) ^ rk[43];
 }
+
+#if R6_SPLIT
+/* Lane-group split AES (round 3).  Four tables T_t = ror(Te0, 8t), 16 copies each: copy c of T_t is dword 16t + c
+ * of every 256-byte row, so it sits in bank (16t + c) mod 32 of a ds_read_b32 (MI355X_MICROARCH.md LDS table).
+ * Lanes l (c = l % 16) form group A (bit 4 of l clear) and group B (set): in every lookup A reads T_t and B T_t+1,
+ * so the 16 A lanes and the 16 B lanes of a 32-lane half meet 32 different banks.  B pays for reading the "wrong"
+ * table by holding its state rotated: after round r its register j holds ror(s_(j + rho_r), 8 eps_r) (rho, eps
+ * below), which one uniform instruction stream keeps consistent -- the byte K of register a that a lookup takes is,
+ * for B, real byte K + eps of s_(a + rho), and T_t+1 supplies the real term rotated by the same amount for all four
+ * terms of a column.  B's round keys are permuted to its representation once per key schedule, and the output
+ * words are brought back by one v_perm each.  Against the two-table layout (Te0, Te2 x 32 copies) this removes the
+ * four rotates of every round (72 issue slots per block) for four v_perm (8).  Checked on the CPU against FIPS-197
+ * (tests/test_r6_split_model.py restates it). */
+/* lookup: byte 1 of the address <- byte K of v, byte 0 <- byte I of the lane's base word (copy + table offset) */
+template <int K, int I>
+DEVI uint32_t r6_ld(uint32_t v, uint32_t base) {
+    const uint32_t a = __builtin_amdgcn_perm(v, base, 0x0c0c0000u | ((4u + K) << 8) | I);
+    return *(const uint32_t *)((const uint8_t *)r6_te + a);
+}
+/* B's representation (rho, eps) after round r = 0..10 */
+__device__ constexpr int R6_RHO[11] = {0, 0, 1, 3, 2, 2, 3, 1, 0, 0, 1};
+__device__ constexpr int R6_EPS[11] = {0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 1};
+
+DEVI void aes128_expand_split(const r6_lds &S, const uint32_t key[4], uint32_t rk[44]) {
+    const uint32_t rcon[10] = {0x01000000u, 0x02000000u, 0x04000000u, 0x08000000u, 0x10000000u,
+                               0x20000000u, 0x40000000u, 0x80000000u, 0x1b000000u, 0x36000000u};
+    rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint32_t t = rk[4 * i + 3];
+        /* byte p of SubWord(RotWord(t)) = S[byte p-1 of t], from a table holding S at byte p: base byte 1-p names
+         * T_1-p for A (S at bytes p+1, p) and T_2-p for B (S at bytes p, p-1) */
+        const uint32_t sw = perm(r6_ld<2, 2>(t, S.base), r6_ld<1, 3>(t, S.base), 0x07020c0cu) |
+                            perm(r6_ld<0, 0>(t, S.base), r6_ld<3, 1>(t, S.base), 0x0c0c0500u);
+        rk[4 * i + 4] = rk[4 * i] ^ sw ^ rcon[i];
+        rk[4 * i + 5] = rk[4 * i + 1] ^ rk[4 * i + 4];
+        rk[4 * i + 6] = rk[4 * i + 2] ^ rk[4 * i + 5];
+        rk[4 * i + 7] = rk[4 * i + 3] ^ rk[4 * i + 6];
+    }
+    /* group B: round r's key word j = ror(rk[4r + (j + rho_r) % 4], 8 eps_r); one v_perm per word (A: identity) */
+    const bool gb = (S.base & 0x40u) != 0u;             /* byte 0: T_0 (A) or T_1 (B) */
+    const uint32_t sk[4] = {gb ? 0x03020100u : 0x07060504u, gb ? 0x00030201u : 0x07060504u,
+                            gb ? 0x01000302u : 0x07060504u, gb ? 0x02010003u : 0x07060504u};
+#pragma unroll
+    for (int r = 1; r <= 10; r++) {
+        if (R6_RHO[r] == 0 && R6_EPS[r] == 0) continue;
+        const uint32_t k0 = rk[4 * r], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        const uint32_t kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) rk[4 * r + j] = perm(kk[j], kk[(j + R6_RHO[r]) & 3], sk[R6_EPS[r]]);
+    }
+}
+
+/* One inner round as an asm block: the 16 lookups issued back to back (column by column), then each column's two
+ * three-way XORs (v_bitop3 0x96) behind the wait that covers its four reads.  LLVM's schedule of the same dataflow keeps 1-2 reads in flight
+ * per wait (the kernel sits at its VGPR limit) and exposes the LDS latency several times per round.  The block
+ * ends with every read consumed, so no LDS operation of it is in flight for the compiler's own waits. */
+#ifndef R6_ASM_ROUND
+#define R6_ASM_ROUND 1
+#endif
+#define R6_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
+DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
+                       uint32_t k1, uint32_t k2, uint32_t k3) {
+    uint32_t t[16];
+#define R6L(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
+    asm volatile(
+        /* column 0: s0 t0, s1 t1, s2 t2, s3 t3;  column 1: s1, s2, s3, s0;  column 2: s2, s3, s0, s1;  column 3 */
+        R6L(4, 0, 25) R6L(5, 1, 26) R6L(6, 2, 27) R6L(7, 3, 28)
+        R6L(8, 1, 25) R6L(9, 2, 26) R6L(10, 3, 27) R6L(11, 0, 28)
+        R6L(12, 2, 25) R6L(13, 3, 26) R6L(14, 0, 27) R6L(15, 1, 28)
+        R6L(16, 3, 25) R6L(17, 0, 26) R6L(18, 1, 27) R6L(19, 2, 28)
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
+        "v_bitop3_b32 %0, %4, %7, %21 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_bitop3_b32 %8, %8, %9, %10 bitop3:0x96\n\t"
+        "v_bitop3_b32 %1, %8, %11, %22 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_bitop3_b32 %12, %12, %13, %14 bitop3:0x96\n\t"
+        "v_bitop3_b32 %2, %12, %15, %23 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_bitop3_b32 %16, %16, %17, %18 bitop3:0x96\n\t"
+        "v_bitop3_b32 %3, %16, %19, %24 bitop3:0x96"
+        : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]),
+          "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
+          "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
+        : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(R6_SEL(0)), "s"(R6_SEL(1)), "s"(R6_SEL(2)),
+          "s"(R6_SEL(3))
+        : "memory");
+#undef R6L
+}
+
+DEVI void aes128_encrypt_split(const r6_lds &S, const uint32_t rk[44], uint32_t s0, uint32_t s1, uint32_t s2,
+                               uint32_t s3, uint32_t out[4]) {
+    uint32_t s[4] = {s0 ^ rk[0], s1 ^ rk[1], s2 ^ rk[2], s3 ^ rk[3]};
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        if (R6_ASM_ROUND) {
+            r6_round_asm(s[0], s[1], s[2], s[3], S.base, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3]);
+            continue;
+        }
+        uint32_t n[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            n[j] = xor3(xor3(r6_ld<3, 0>(s[j], S.base), r6_ld<2, 1>(s[(j + 1) & 3], S.base),
+                             r6_ld<1, 2>(s[(j + 2) & 3], S.base)),
+                        r6_ld<0, 3>(s[(j + 3) & 3], S.base), rk[4 * r + j]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) s[j] = n[j];
+    }
+    /* last round: byte p of word j <- S[byte p of s_(j+3-p)] (B: of its rotated registers) through base byte 1-p
+     * (A: T_1-p, B: T_2-p, both with S at byte p), combined as before */
+    uint32_t acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        acc[j] = (perm(r6_ld<3, 2>(s[j], S.base), r6_ld<2, 3>(s[(j + 1) & 3], S.base), 0x07020c0cu) |
+                  perm(r6_ld<1, 0>(s[(j + 2) & 3], S.base), r6_ld<0, 1>(s[(j + 3) & 3], S.base), 0x0c0c0500u)) ^
+                 rk[40 + j];
+    /* B's word j holds ror(out[j + 1], 8): out[j] = rol(acc[j - 1], 8).  The selector is derived from base here
+     * rather than kept in a register across the round (the kernel sits at its 168-VGPR limit) */
+    const uint32_t selr = (S.base & 0x40u) ? 0x02010003u : 0x07060504u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) out[j] = perm(acc[j], acc[(j + 3) & 3], selr);
+}
+#define R6_EXPAND aes128_expand_split
+#define R6_ENCRYPT aes128_encrypt_split
+#else
+#define R6_EXPAND aes128_expand_te
+#define R6_ENCRYPT aes128_encrypt_te
+#endif
 
 /* SHA-512 over 32 BE words held as two 16-word halves; state as 16 BE words (hi, lo pairs) */
 DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const uint32_t hi[16]) {
@@ -300,9 +445,9 @@ DEVI void r6_load_k(const r6_lds &S, uint32_t len, uint32_t K[8]) {
 DEVI uint32_t r6_family(const r6_lds &S, uint32_t len) {
     uint32_t K[8], rk[44], v[4], y[4];
     r6_load_k(S, len, K);
-    aes128_expand_te(S, K, rk);
+    R6_EXPAND(S, K, rk);
     r6_read16(S, 0u, v);
-    aes128_encrypt_te(S, rk, v[0] ^ K[4], v[1] ^ K[5], v[2] ^ K[6], v[3] ^ K[7], y);
+    R6_ENCRYPT(S, rk, v[0] ^ K[4], v[1] ^ K[5], v[2] ^ K[6], v[3] ^ K[7], y);
     uint32_t sum = __builtin_amdgcn_sad_u8(y[0], 0u, 0u);
     sum = __builtin_amdgcn_sad_u8(y[1], 0u, sum);
     sum = __builtin_amdgcn_sad_u8(y[2], 0u, sum);
@@ -323,7 +468,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
     r6_load_k(S, len, K);
     /* AES-128 key K[0:16], iv K[16:32] (:259-261) */
     uint32_t rk[44];
-    aes128_expand_te(S, K, rk);
+    R6_EXPAND(S, K, rk);
     uint32_t prev[4] = {K[4], K[5], K[6], K[7]};
     uint32_t hs[16], half[16];
     if (hsel == 0) {
@@ -351,7 +496,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
             } else {
                 r6_read16(S, o, v);
             }
-            aes128_encrypt_te(S, rk, v[0] ^ prev[0], v[1] ^ prev[1], v[2] ^ prev[2], v[3] ^ prev[3], y);
+            R6_ENCRYPT(S, rk, v[0] ^ prev[0], v[1] ^ prev[1], v[2] ^ prev[2], v[3] ^ prev[3], y);
 #pragma unroll
             for (int k = 0; k < 4; k++) { prev[k] = y[k]; w[4 * q + k] = y[k]; }
             o += 16u;
@@ -445,6 +590,9 @@ struct r6_shared {
                                                  64-bit start was spilled to scratch (SGPR pressure) */
     uint8_t sdig[DPRF_MAX_RANGE_LEN];         /* base-cslen digits of the launch's first index          */
     uint16_t stage[R6_LANES / 64][64];        /* per wave: the slot ids of the batch it claimed         */
+    unsigned long long idle_t0[R6_LANES / 64];  /* per wave: wall clock when it first found nothing queued, 0 while
+                                                 it finds work (in LDS: a 64-bit value held in registers across the
+                                                 loop was one of the split-AES build's spills) */
     uint32_t state[R6_MAX_SLOTS];             /* len | bs << 8 | round << 16                            */
     uint32_t cand[R6_MAX_SLOTS];              /* candidate offset within the launch, R6_IDLE when none  */
 };
@@ -460,7 +608,21 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
         S.lanebase = (t & 63u) << 2;
     }
     S.lanec = (lane & (R6_TE_COPIES - 1u)) << 2;
+#if R6_SPLIT
+    /* copy c = lane % 16 in every byte; table offsets 64 t: A (lane bit 4 clear) T_t / B T_t+1 for lookup t */
+    const uint32_t c4 = S.lanec * 0x01010101u;
+    const bool gb = (lane & 16u) != 0u;
+    S.base = c4 + (gb ? 0x00c08040u : 0xc0804000u);
+#endif
     return S;
+}
+
+/* the lane index as an opaque value (LLVM cannot hoist it): used where a lane-derived value would otherwise be held
+ * across the persistent loop -- at the kernel's VGPR limit such values were what the register allocator spilled */
+DEVI uint32_t opaque_lane() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
 }
 
 DEVI uint32_t lds_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -615,21 +777,21 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     }
     __syncthreads();
     R6T_DECL
-    bool idling = false;
-    uint64_t idle_t0 = 0;
+    if (lane == 0) sh->idle_t0[wave] = 0ull;
     for (;;) {
         uint32_t slot;
-        const uint32_t n = r6_claim(sh, lane, wave, &slot);
+        const uint32_t n = r6_claim(sh, opaque_lane(), wave, &slot);
         if (n == 0) {
             if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
             /* watchdog on the constant-rate wall clock: a wave that has found nothing queued for idle_ticks
              * (host: 10 s; a whole launch is ~3 s and the drain after the cursor runs dry tens of ms) gives up
              * and flags the launch instead of hanging the device; the host turns the flag into an error */
-            const uint64_t now = wall_clock64();
-            if (!idling) {
-                idling = true;
-                idle_t0 = now;
-            } else if (now - idle_t0 > idle_ticks) {
+            const uint64_t now = wall_clock64() | 1ull;                 /* never 0: 0 marks "not idling" */
+            const unsigned long long t0 = lds_load64(&sh->idle_t0[wave]);
+            if (t0 == 0ull) {
+                if (lane == 0) __hip_atomic_store(&sh->idle_t0[wave], (unsigned long long)now, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (now - t0 > idle_ticks) {
                 if (lane == 0) atomicOr(&R->pad_, 1u);
                 break;
             }
@@ -637,13 +799,13 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             R6T_MARK(t_wait)
             continue;
         }
-        idling = false;
+        if (lane == 0) __hip_atomic_store(&sh->idle_t0[wave], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef DPRF_R6_TIMING
         t_nb++;
         t_part += n;
 #endif
         if (slot != R6_IDLE) {
-            const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, lane);
+            const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
             const uint32_t st = sh->state[slot];
             const uint32_t len = st & 0xffu, hs = st >> 30;
             uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
@@ -663,7 +825,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
                 /* the finishing lanes of the batch take their next candidates together */
-                more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, lane));
+                more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
                 if (!more) atomicSub(&sh->live, 1u);
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);

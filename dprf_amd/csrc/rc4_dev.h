@@ -112,16 +112,34 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
 }
 
 /* The same KSA as one generated inline-asm block (rc4_ksa_asm.h, tools/gen_rc4_ksa_asm.py: the schedule above in
- * 11 VALU instructions per group of two steps instead of the 16-17 LLVM emits, byte selects as SDWA operands).
+ * 11 VALU instructions per group of two steps instead of the 16-17 LLVM emits, byte selects as SDWA operands, and
+ * -- RC4_KSA_KB_CTR, round 3 -- the compare positions i0 / i1 counted in byte 3 of j itself).
  * sbase: LDS address of the wave's 16 KiB area, low 16 bits zero (the SDWA byte-1 insert of the S[j] address
  * overwrites bits 8-15 of lanebase; the caller checks); lanebase = sbase + 4 * lane.  Writes the identity itself
- * and returns with no LDS operation in flight. */
+ * and returns with no LDS operation in flight.  kb: the key registers rc4_kb_init makes. */
+#ifndef RC4_KSA_KB_CTR                   /* headers generated before the j counter */
+#define RC4_KSA_KB_CTR 0
+#define RC4_KSA_NKR_5 5
+#endif
+template <int NK> struct rc4_nkr { static constexpr int v = NK == 5 ? RC4_KSA_NKR_5 : NK; };
+
+/* Key registers of the asm KSA from the LE-packed key k[4]: register q holds key byte q % NK in byte 0; with the j
+ * counter bytes 1-2 are zero and byte 3 is the counter's step for the parity of the positions it serves (+3 after
+ * an even step, -1 after an odd one: byte 3 of j is then i1 after step i0 and i0 after step i1).  Only byte 0 changes
+ * when a caller XORs a pass constant < 256 into every register (R3/R4's key ^ x). */
 template <int NK>
-DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
-    static_assert(NK == 5 || NK == 16, "rc4_ksa_asm.h holds the 5- and 16-byte key schedules");
-    uint32_t kb[NK];
+DEVI void rc4_kb_init(const uint32_t k[4], uint32_t kb[rc4_nkr<NK>::v]) {
 #pragma unroll
-    for (int q = 0; q < NK; q++) kb[q] = k[q >> 2] >> (8 * (q & 3));    /* only the low byte is used */
+    for (int q = 0; q < rc4_nkr<NK>::v; q++) {
+        const int p = q % NK;
+        const uint32_t b = k[p >> 2] >> (8 * (p & 3));
+        kb[q] = RC4_KSA_KB_CTR ? ((b & 0xffu) | ((q & 1) ? 0xff000000u : 0x03000000u)) : b;
+    }
+}
+
+template <int NK>
+DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc4_nkr<NK>::v]) {
+    static_assert(NK == 5 || NK == 16, "rc4_ksa_asm.h holds the 5- and 16-byte key schedules");
     uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s, wn;
     uint64_t c0, c1, c2, c3, h0;                       /* SGPR pairs of the prefetch variant (A/B headers) */
     /* the identity by ds_write_b128: lane l writes row 4t + l/16, bytes 16 (l%16) .. +16, for t = 0..15, first
@@ -133,22 +151,35 @@ DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
 #define RC4_KSA_OUTS                                                                                               \
     "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st), "=&s"(m0s),   \
         "=&v"(wn), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(h0)
+#define RC4_KSA_INS "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0)
+#define KB(q) "v"(kb[(q) % rc4_nkr<NK>::v])
     if constexpr (NK == 16) {
         asm volatile(RC4_KSA_ASM_16
                      : RC4_KSA_OUTS
-                     : "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0), "v"(kb[0]), "v"(kb[1]), "v"(kb[2]),
-                       "v"(kb[3]), "v"(kb[4]), "v"(kb[(5) % NK]), "v"(kb[(6) % NK]), "v"(kb[(7) % NK]),
-                       "v"(kb[(8) % NK]), "v"(kb[(9) % NK]), "v"(kb[(10) % NK]), "v"(kb[(11) % NK]),
-                       "v"(kb[(12) % NK]), "v"(kb[(13) % NK]), "v"(kb[(14) % NK]), "v"(kb[(15) % NK])
+                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9), KB(10),
+                       KB(11), KB(12), KB(13), KB(14), KB(15)
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     } else {
+        /* the operand count is checked where the template is defined: the variant is chosen by the preprocessor */
         asm volatile(RC4_KSA_ASM_5
                      : RC4_KSA_OUTS
-                     : "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0), "v"(kb[0]), "v"(kb[1 % NK]),
-                       "v"(kb[2 % NK]), "v"(kb[3 % NK]), "v"(kb[4 % NK])
+#if RC4_KSA_NKR_5 == 10
+                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9)
+#else
+                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4)
+#endif
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     }
+#undef KB
+#undef RC4_KSA_INS
 #undef RC4_KSA_OUTS
+}
+
+template <int NK>
+DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
+    uint32_t kb[rc4_nkr<NK>::v];
+    rc4_kb_init<NK>(k, kb);
+    rc4_ksa_asm_kb<NK>(sbase, lanebase, kb);
 }
 
 /* R2 (one KSA per candidate) runs the same rc4_ksa; its round-1 one-step-ahead KSA (S[j] and S[i+1] read

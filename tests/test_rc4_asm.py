@@ -32,22 +32,30 @@ def ref_ksa(key, n):
     return S
 
 
-def emulate(prog, keys, nk, sbase=0):
-    """Run the block for 64 lanes; keys[l] = the lane's key bytes.  Returns the 64 S-boxes."""
+def emulate(prog, keys, nk, sbase=0, text=None):
+    """Run the block for 64 lanes; keys[l] = the lane's key bytes.  Returns the 64 S-boxes.  text: the header the
+    block comes from (its RC4_KSA_KB_CTR says how the kernel fills the key registers)."""
     lds = np.zeros(sbase + 16384, dtype=np.uint8)
     lane = np.arange(LANES, dtype=np.uint64)
     regs = {}
     sregs = {"m0": 0}
     kb = []
-    for q in range(nk):
-        w = np.array([int.from_bytes(bytes(k[(q & ~3):(q & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
+    ctr = re.search(r"#define RC4_KSA_KB_CTR (\d)", text or "")
+    ctr = bool(ctr and ctr.group(1) == "1")
+    nkr = 10 if (ctr and nk == 5) else nk
+    for q in range(nkr):
+        p = q % nk
+        w = np.array([int.from_bytes(bytes(k[(p & ~3):(p & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
                      dtype=np.uint64)
-        kb.append(w >> np.uint64(8 * (q & 3)))            # garbage above byte 0, as the kernel passes them
+        w = w >> np.uint64(8 * (p & 3))                   # garbage above byte 0, as the kernel passes raw registers
+        if ctr:                                           # rc4_kb_init: key byte | j-counter step in byte 3
+            w = (w & np.uint64(0xff)) | np.uint64(0xff000000 if q & 1 else 0x03000000)
+        kb.append(w)
     l4 = 4 * lane
     vin = {"%16": sbase + l4, "%17": sbase,
            "%18": sbase + ((l4 >> np.uint64(6)) << np.uint64(8)) + ((l4 & np.uint64(60)) << np.uint64(2)),
            "%19": 0x1010101010101010, "%20": np.uint64(0x03020100) + np.uint64(0x04040404) * (l4 >> np.uint64(6))}
-    for q in range(nk):
+    for q in range(nkr):
         vin["%%%d" % (21 + q)] = kb[q]
     masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
     vcc = np.zeros(LANES, dtype=bool)
@@ -110,8 +118,9 @@ def emulate(prog, keys, nk, sbase=0):
         elif op == "v_cmp_eq_u32_sdwa":
             assert "src0_sel:BYTE_0" in ln
             src1 = a[2].split()[0]
-            if src1.startswith("%") and src1 not in sregs and src1 not in vin:      # a VGPR, byte-selected
-                sh1 = {"BYTE_0": 0, "BYTE_1": 8}[re.search(r"src1_sel:(\w+)", ln).group(1)]
+            if src1.startswith("%") and src1 not in sregs and (src1 not in vin or not isinstance(vin[src1], int)):
+                # a VGPR, byte-selected (BYTE_3 of j: the position counter)
+                sh1 = {"BYTE_0": 0, "BYTE_1": 8, "BYTE_3": 24}[re.search(r"src1_sel:(\w+)", ln).group(1)]
                 r = (v(a[1]) & np.uint64(0xff)) == ((v(src1) >> np.uint64(sh1)) & np.uint64(0xff))
             else:
                 r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(src1))
@@ -176,19 +185,21 @@ def emulate(prog, keys, nk, sbase=0):
 def test_generated_ksa_equals_rc4(nk):
     if not os.path.exists(HDR):
         pytest.skip("rc4_ksa_asm.h not generated")
-    prog = program(nk)
+    text = open(HDR).read()
+    prog = program(nk, text)
     rng = random.Random(nk)
     for trial in range(3):
         keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
         if trial == 1:
             keys[0] = [0] * 16                     # j == i collisions early on
             keys[1] = [1] * 16
-        got = emulate(prog, keys, nk)
+        got = emulate(prog, keys, nk, text=text)
         for l_ in range(LANES):
             assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
 
 
-@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity"])
+@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
+                                  "--jctr"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""
@@ -200,7 +211,7 @@ def test_schedule_variants_equal_rc4(flag):
         rng = random.Random(nk + 100)
         keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
         keys[0], keys[1], keys[2] = [0] * 16, [1] * 16, [2] * 16
-        got = emulate(program(nk, text), keys, nk)
+        got = emulate(program(nk, text), keys, nk, text=text)
         assert all(got[l_] == ref_ksa(keys[l_], nk) for l_ in range(LANES)), (flag, nk)
 
 

@@ -42,6 +42,8 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     group and repaired for its S[j] stores)
        tools/gen_rc4_ksa_asm.py --salu-consts > <variant header>  (A/B, round-3 first version: compare constants
                                                                     through two s_movk per group)
+       tools/gen_rc4_ksa_asm.py --jctr > <variant header>         (A/B: i0 / i1 counted in byte 3 of j, key registers
+                                                                    carrying the counter steps: 603 vs 612 M, slower)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
                                                                     64-bit adds: 612 -> 595 M, the b128 stores cost
                                                                     more LDS time than the instructions they save)
@@ -55,7 +57,13 @@ def pos(i):
     return ((i >> 2) << 8) + (i & 3)
 
 
-def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False):
+def nkr_of(nk, jctr):
+    """key registers the block reads: with the j counter every register must serve one step parity, so the 5-byte
+    key is passed as 10 registers (key byte i % 5 with the counter step of i's parity)"""
+    return 10 if (jctr and nk % 2) else nk
+
+
+def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -63,7 +71,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
     #           the b128 identity's data quad is the clobbered v[60:63] (a register tuple operand cannot be split)
     J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, IA, C16, D0 = (
         "%%%d" % k for k in range(21))
-    KB = ["%%%d" % (21 + k) for k in range(nk)]
+    nkr = nkr_of(nk, jctr)
+    KB = ["%%%d" % (21 + k) for k in range(nkr)]
     if prefetch:
         return ksa_prefetch(nk, J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, KB)
     out = []
@@ -73,10 +82,15 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
         identity_b128(e, IA, C16, D0)
     else:
         identity(e, M, M0S, SB)
-    e("v_mov_b32 %s, 0" % J)
+    # jctr: byte 3 of j counts positions (the key registers carry +3 / -1 in byte 3 for even / odd steps), so after
+    # step 0 of group q it is i1 and after step 1 it is i0: both compares read it from j itself.  Bytes 1-2 absorb the
+    # carries and W's byte 1 (at most 128 x 0x101 per KSA < 2^16: nothing reaches byte 3).
+    e("v_mov_b32 %s, %s" % (J, "0xfe000000" if jctr else "0"))
     e("v_mov_b32 %s, 0x100" % W)         # group 0 = S[0] | S[1] << 8 of the identity
     IC = WN                              # vconst: (i0, i1) of the group in bytes 0, 1 of a VGPR, from the first
     FIRST_IC = 32 if vconst else 0       # group whose i1 is past the inline constants (0..64)
+    if jctr:
+        vconst = False
     if vconst:
         e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
     def merge(q):
@@ -90,8 +104,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
         i0, i1 = 2 * q, 2 * q + 1
         if q > 0:
             e("s_waitcnt lgkmcnt(%d)" % (0 if late_merge else 1))
-        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
-        if not vconst:
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nkr]))
+        if not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i1))
         e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
@@ -103,6 +117,10 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_write_b8 %s, %s" % (A0, W))
             e("s_movk_i32 %s, %d" % (ST, i0))
+        elif jctr:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_3" % (J, J))
+            e("ds_read_u8 %s, %s" % (X0, A0))
+            e("ds_write_b8 %s, %s" % (A0, W))
         elif vconst:
             if q < FIRST_IC:
                 e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i1))
@@ -116,8 +134,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("ds_write_b8 %s, %s" % (A0, W))
         e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
           % (V1, W, W))
-        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
-        if not early_read and not vconst:
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nkr]))
+        if not early_read and not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i0))
         e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
@@ -125,6 +143,9 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
         if early_read:
             e("ds_read_u8 %s, %s" % (X1, A1))
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
+        elif jctr:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_3" % (J, J))
+            e("ds_read_u8 %s, %s" % (X1, A1))
         elif vconst:
             if q < FIRST_IC:
                 e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i0))
@@ -259,11 +280,18 @@ def main():
     pre = "--prefetch" in sys.argv
     vconst = "--salu-consts" not in sys.argv
     b128 = "--b128-identity" in sys.argv
+    # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
+    # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
+    jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
     print("/* rc4_ksa_asm.h -- GENERATED by tools/gen_rc4_ksa_asm.py (see there for the schedule); do not edit. */")
     print("#ifndef DPRF_RC4_KSA_ASM_H")
     print("#define DPRF_RC4_KSA_ASM_H")
+    print("/* key registers: 1 = byte 0 the key byte, bytes 1-2 zero, byte 3 the j-counter step (+3 even / -1 odd")
+    print("   positions); 0 = the key byte in byte 0, anything above it.  RC4_KSA_NKR_5: registers of the 5-byte key */")
+    print("#define RC4_KSA_KB_CTR %d" % (1 if jctr else 0))
+    print("#define RC4_KSA_NKR_5 %d" % nkr_of(5, jctr))
     for nk in KEYLENS:
-        lines = ksa(nk, early, late, pre, vconst and not early, b128)
+        lines = ksa(nk, early, late, pre, vconst and not early, b128, jctr)
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
