@@ -15,9 +15,8 @@ import sys
 # Kernel name (demangled; an entry with template arguments wins over the bare name) -> the most scratch it may
 # use, bytes/lane.  Every kernel must appear here: an unknown kernel fails the gate too.
 SCRATCH_LIMIT = {
-    # list-mode R6 (client payloads, not a benchmarked configuration): the per-lane block offset and byte
-    # selector (wave-uniform in range mode) leave one 64-bit value spilled inside the SHA-512 compression
-    "k_pdf_r6<1>": 16,
+    # every kernel at 0 B/lane since round 3 (list-mode R6 had 16 until the persistent loop stopped holding its lane
+    # index and the watchdog's 64-bit timestamp in registers: dprf_kernels_r6.hip opaque_lane, idle_t0 in LDS)
     "k_office_kdf": 0,
     "k_office_check": 0,
     "k_odt_kdf": 0,

@@ -3,6 +3,6 @@ ab() { W=$1; shift; for V in "$@"; do
   if [ "$V" = "base" ]; then L=$PWD/dprf_amd/libdprf.so; else L=$PWD/build/ab/libdprf_$V.so; fi
   DPRF_LIB=$L timeout -k 5 150 python bench.py --workload $W --no-side --cpu-seconds 0 --steps 3 | python -c "import json,sys; d=json.load(sys.stdin); print('$W $V', d['value'], d['roofline']['frac'], d['roofline']['kernel_avg_ms'])" || exit 1
 done; }
-DPRF_LIB=$PWD/build/ab/libdprf_r6split2.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_r6split2.log 2>&1
-echo "tests rc=$? $(tail -1 gpurun_out/gputests_r6split2.log)"
-ab pdf_r6 r6old r6old2 r6split2 r6split2c r6old r6old2 r6split2 r6split2c
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_split3.log 2>&1
+echo "tests rc=$? $(tail -1 gpurun_out/gputests_split3.log)"
+ab pdf_r6 base r6split2 r6old base r6split2 r6old
