@@ -433,7 +433,7 @@ def main():
                           "valu_floor_frac": (sm["per_launch"] * work.per_candidate(skey)
                                               / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak),
                           "call_overhead": sm["call_overhead"]}
-            if work.BOUND.get(skey) == "lds":
+            if skey in work.LDS_CYCLES:             # RC4 formats: the modelled LDS-array share (~ rocprof LdsUtil)
                 side[name]["lds_cycle_frac"] = work.lds_frac(
                     skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
             pc = pmc_summary(name, build)

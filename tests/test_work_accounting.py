@@ -60,18 +60,31 @@ def test_pdf_r6_mean_counts(oracle, streams):
 
 
 def test_lds_cycle_model():
-    # per wave: R3/R4 20 x (64 addtid x 2 + 256 x (S[j] read 2 + S[j] store 4) + 128 u16 stores of the
-    # group-deferred S[i] sides x 4 + 127 u16 group reads x 2 + PRGA-2 in registers: 5 reads x 2) + the key
-    # hand-off of a batch (4 dword stores x 4 + 4 dword reads x 2)
-    assert work.LDS_CYCLES["pdf_r34"] * 64 == (20 * (64 * 2 + 256 * 6 + 128 * 4 + 127 * 2 + 5 * 2)
-                                              + 4 * 4 + 4 * 2)
+    # LDS-array cycles per wave: R3/R4 20 x (831 KSA ops x 2 + PRGA-2 in registers: 5 reads x 2) + the key hand-off
+    # of a batch (4 dword stores + 4 dword reads, 2 cycles each)
+    assert work.LDS_CYCLES["pdf_r34"] * 64 == 20 * ((64 + 256 + 256 + 128 + 127) * 2 + 5 * 2) + 8 * 2
     # R2: the same KSA + 4 PRGA bytes x (3 reads + 2 stores) + the key hand-off
-    assert work.LDS_CYCLES["pdf_r2"] * 64 == (64 * 2 + 256 * 6 + 128 * 4 + 127 * 2 + 4 * (3 * 2 + 2 * 4)
-                                             + 4 * 4 + 4 * 2)
+    assert work.LDS_CYCLES["pdf_r2"] * 64 == (64 + 256 + 256 + 128 + 127) * 2 + 4 * 5 * 2 + 8 * 2
     assert work.lds_frac("odt", 1e6) is None
     assert abs(work.lds_frac("pdf_r34", 1e6) - 1e6 * work.LDS_CYCLES["pdf_r34"] / (256 * 2.4e9)) < 1e-12
-    for fmt in work.LDS_CYCLES:
-        assert work.BOUND[fmt] == "lds"
+
+
+def test_lds_cycle_model_matches_rocprof_lds_util():
+    """The LDS-array model against rocprof's LdsUtil (SQ_LDS_IDX_ACTIVE per CU per cycle, ROCm's derived formula)
+    of the same kernel on MI355X, at the candidate rate and clock of that profiled run (profiles/*_r03d.json):
+    within 10 % (the verdict's bar; measured: within 1.5 %)."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for fmt in ("pdf_r34", "pdf_r2"):
+        d = json.load(open(os.path.join(root, "profiles", "prof_%s_r03d.json" % fmt)))
+        (pd,) = [v["per_dispatch"] for k, v in d["counters"].items() if "k_pdf_r24" in k]
+        cycles = pd["GRBM_GUI_ACTIVE"] / 8.0                    # per XCD = per CU
+        lds_util = pd["SQ_LDS_IDX_ACTIVE"] / 256.0 / cycles
+        rate = d["bench_under_profiler"]["value"]
+        clock = d["bench_under_profiler"]["roofline"]["rocprof"]["effective_clock_GHz"] * 1e9
+        model = rate * work.LDS_CYCLES[fmt] / (256 * clock)
+        assert abs(model - lds_util) / lds_util < 0.10, (fmt, model, lds_util)
 
 
 def test_lds_instruction_count_matches_rocprof():
