@@ -622,6 +622,16 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #endif
 #define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
 #define R6_CLASSES 6
+/* Deferred candidate starts (A/B option, round 3): a slot whose candidate finishes is queued in a seventh queue
+ * instead of starting its next candidate inside the round's batch, where the SHA-256 of a new candidate runs for the
+ * one or two lanes that finished.  A wave takes that queue as its batch once R6_START_BATCH slots wait in it (or when
+ * nothing else is queued).  Measured on MI355X: 3.674 vs 3.683 M cand/s at 16 (the build spills 16 B/lane), so the
+ * lane idleness left (VALUUtilization 0.947) is not these starts; off by default. */
+#ifndef R6_START_BATCH
+#define R6_START_BATCH 0
+#endif
+#define R6_QUEUES (R6_CLASSES + 1)
+#define R6_START_Q R6_CLASSES
 #define R6_MAP_WORDS ((R6_MAX_SLOTS + 31) / 32)
 #define R6_IDLE 0xffffffffu
 #ifndef R6_WATCHDOG_S
@@ -629,8 +639,8 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #endif
 
 struct r6_shared {
-    uint32_t map[R6_CLASSES][R6_MAP_WORDS];   /* queued slots of each class, one bit per slot          */
-    uint32_t count[R6_CLASSES];               /* queued slots per class (a hint for picking the class) */
+    uint32_t map[R6_QUEUES][R6_MAP_WORDS];    /* queued slots of each class (+ the start queue), a bit per slot */
+    uint32_t count[R6_QUEUES];                /* queued slots per queue (a hint for picking one)       */
     uint32_t live;                            /* slots holding a candidate                             */
     uint32_t nslots, te_slots, ncand;
     const uint32_t *slots;                    /* e.slots, e.lens (list mode), likewise */
@@ -733,14 +743,19 @@ DEVI void r6_push(r6_shared *sh, const r6_lds &S, uint32_t slot) {
  * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
  * order up to 64 in total, clear exactly the bits they chose (atomicAnd returns what they got when another
  * wave raced them), and the ids are handed out through the wave's stage row. */
-DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot) {
-    const uint32_t cnt = lane < R6_CLASSES ? lds_load(&sh->count[lane]) : 0u;
+DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t *queue) {
+    const uint32_t cnt = lane < R6_QUEUES ? lds_load(&sh->count[lane]) : 0u;
     uint32_t best = R6_CLASSES, bc = 0;
 #pragma unroll
     for (int c = 0; c < R6_CLASSES; c++) {
         const uint32_t v = __builtin_amdgcn_readlane(cnt, c);
         if (v > bc) { bc = v; best = c; }
     }
+    if (R6_START_BATCH) {
+        const uint32_t vs = __builtin_amdgcn_readlane(cnt, R6_START_Q);
+        if (vs >= R6_START_BATCH || (bc == 0 && vs > 0)) { bc = vs; best = R6_START_Q; }
+    }
+    *queue = best;
     if (bc == 0) return 0;
     const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
     const uint32_t pc = __builtin_popcount(w);
@@ -806,8 +821,8 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         r6_te[x * (R6_TE_ROW_BYTES / 4) + c] = ror32(T->te0[x], (R6_TABLES == 2 ? 16 : 8) * t);
     }
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
-    for (uint32_t k = tid; k < R6_CLASSES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
-    if (tid < R6_CLASSES) sh->count[tid] = 0u;
+    for (uint32_t k = tid; k < R6_QUEUES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
+    if (tid < R6_QUEUES) sh->count[tid] = 0u;
     if (tid < DPRF_MAX_RANGE_LEN) sh->sdig[tid] = e.sdig[tid];
     if (tid == 0) {
         sh->live = 0u;
@@ -829,8 +844,8 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     R6T_DECL
     if (lane == 0) sh->idle_t0[wave] = 0ull;
     for (;;) {
-        uint32_t slot;
-        const uint32_t n = r6_claim(sh, opaque_lane(), wave, &slot);
+        uint32_t slot, queue;
+        const uint32_t n = r6_claim(sh, opaque_lane(), wave, &slot, &queue);
         if (n == 0) {
             if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
             /* watchdog on the constant-rate wall clock: a wave that has found nothing queued for idle_ticks
@@ -854,6 +869,19 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         t_nb++;
         t_part += n;
 #endif
+        if (R6_START_BATCH && queue == R6_START_Q) {
+            /* a batch of slots whose candidates finished: they take their next candidates together (one cursor
+             * atomic for the wave), start them and queue their first rounds, or retire when the cursor is dry */
+            if (slot != R6_IDLE) {
+                const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
+                if (r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane())))
+                    r6_push(sh, S, slot);
+                else
+                    atomicSub(&sh->live, 1u);
+            }
+            R6T_MARK(t_work)
+            continue;
+        }
         if (slot != R6_IDLE) {
             const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
             const uint32_t st = sh->state[slot];
@@ -874,9 +902,17 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     atomicMin(&R->first, idx);
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
-                /* the finishing lanes of the batch take their next candidates together */
-                more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
-                if (!more) atomicSub(&sh->live, 1u);
+                if (R6_START_BATCH) {
+                    /* to the start queue (the slot stays live until it takes a candidate or retires) */
+                    more = false;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    atomicOr(&sh->map[R6_START_Q][slot >> 5], 1u << (slot & 31u));
+                    atomicAdd(&sh->count[R6_START_Q], 1u);
+                } else {
+                    /* the finishing lanes of the batch take their next candidates together */
+                    more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
+                    if (!more) atomicSub(&sh->live, 1u);
+                }
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);
             }
