@@ -318,11 +318,22 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
 
 /* The 64 AES-256 block decryptions per candidate read Td0 14,336 times.  A single 1 KiB Td0 puts
  * random indices of 32 lanes on 32 banks (~3.5-way conflicts: 65 % of this kernel's cycles were bank
- * conflicts, profiles/prof_odt_r01.json).  Here row x of a 64 KiB table holds Td0[x] in 32 dword copies
- * (bytes 0..127, lane l reads copy l%32) and Si[x] in 32 dword copies (bytes 128..255): every lookup is
- * conflict-free and its address is ONE v_perm of the state byte and the lane's copy offset. */
+ * conflicts, profiles/prof_odt_r01.json).  Rounds 1-2 (ODT_SPLIT 0): row x of a 64 KiB table holds Td0[x] in 32
+ * dword copies (bytes 0..127, lane l reads copy l%32) and Si[x] in 32 dword copies (bytes 128..255): every lookup
+ * conflict-free, its address ONE v_perm of the state byte and the lane's copy offset, but three of a column's four
+ * terms rotated (12 v_alignbit per round).
+ * Round 3 (ODT_SPLIT 1): R6's split-table scheme (dprf_kernels_r6.hip aes128_encrypt_split) for the inverse cipher:
+ * four tables Td_t = ror(Td0, 8t) x 16 copies fill the 256-byte rows, lane group A (bit 4 of the lane clear) reads
+ * Td_t and group B Td_t+1 in every lookup (32 different banks per 32-lane half), B keeps its state rotated -- after
+ * inner round r its register j holds ror(s_(j + rho_r), 8 eps_r) with (rho, eps) -> (rho - eps, eps + 1) for the
+ * inverse cipher's column order -- and its round keys are permuted to match; no rotates are left.  Si sits in one
+ * more row (address 0x10000 + x, one v_perm; the last round's 16 byte reads share its banks).
+ * tests/test_odt_split_model.py restates it against FIPS-197. */
+#ifndef ODT_SPLIT
+#define ODT_SPLIT 1
+#endif
 #define ODT_TD_ROW 256
-__shared__ __attribute__((aligned(16))) uint32_t odt_td[256 * ODT_TD_ROW / 4];
+__shared__ __attribute__((aligned(16))) uint32_t odt_td[(256 + ODT_SPLIT) * ODT_TD_ROW / 4];
 
 template <int K>
 DEVI uint32_t tdrep(uint32_t v, uint32_t lanec) {
@@ -356,6 +367,78 @@ DEVI void aes256_decrypt_rep(const uint32_t *dk, const uint32_t in[4], uint32_t 
     out[3] = ((isbrep<3>(s3, lanec) << 24) | (isbrep<2>(s2, lanec) << 16) | (isbrep<1>(s1, lanec) << 8) | isbrep<0>(s0, lanec)) ^ r[3];
 }
 
+#if ODT_SPLIT
+/* B's representation (rho, eps) after inner round r = 0..13 of the inverse cipher */
+__device__ constexpr int ODT_RHO[14] = {0, 0, 3, 1, 2, 2, 1, 3, 0, 0, 3, 1, 2, 2};
+__device__ constexpr int ODT_EPS[14] = {0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3, 0, 1};
+#define ODT_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
+/* One inner round: 16 lookups issued column by column (column j: s_j, s_j-1, s_j-2, s_j-3 for lookups t = 0..3),
+ * then each column's two v_bitop3 behind the wait covering its reads (as r6_round_asm). */
+DEVI void odt_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
+                        uint32_t k1, uint32_t k2, uint32_t k3) {
+    uint32_t t[16];
+#define ODL(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
+    asm volatile(
+        ODL(4, 0, 25) ODL(5, 3, 26) ODL(6, 2, 27) ODL(7, 1, 28)
+        ODL(8, 1, 25) ODL(9, 0, 26) ODL(10, 3, 27) ODL(11, 2, 28)
+        ODL(12, 2, 25) ODL(13, 1, 26) ODL(14, 0, 27) ODL(15, 3, 28)
+        ODL(16, 3, 25) ODL(17, 2, 26) ODL(18, 1, 27) ODL(19, 0, 28)
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
+        "v_bitop3_b32 %0, %4, %7, %21 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_bitop3_b32 %8, %8, %9, %10 bitop3:0x96\n\t"
+        "v_bitop3_b32 %1, %8, %11, %22 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_bitop3_b32 %12, %12, %13, %14 bitop3:0x96\n\t"
+        "v_bitop3_b32 %2, %12, %15, %23 bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_bitop3_b32 %16, %16, %17, %18 bitop3:0x96\n\t"
+        "v_bitop3_b32 %3, %16, %19, %24 bitop3:0x96"
+        : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]),
+          "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
+          "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
+        : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(ODT_SEL(0)), "s"(ODT_SEL(1)), "s"(ODT_SEL(2)),
+          "s"(ODT_SEL(3))
+        : "memory");
+#undef ODL
+}
+/* Si[byte K of v] from the row after the tables (address 0x10000 + x) */
+template <int K>
+DEVI uint32_t odt_si(uint32_t v) {
+    const uint32_t a = __builtin_amdgcn_perm(v, 0x00010000u, 0x0c020000u | (4u + K));
+    return ((const uint8_t *)odt_td)[a];
+}
+/* Group B's round keys in its representation (A: unchanged) -- once per key schedule */
+DEVI void odt_dk_split(uint32_t dk[60], uint32_t base) {
+    const bool gb = (base & 0x40u) != 0u;
+    const uint32_t sk[4] = {gb ? 0x03020100u : 0x07060504u, gb ? 0x00030201u : 0x07060504u,
+                            gb ? 0x01000302u : 0x07060504u, gb ? 0x02010003u : 0x07060504u};
+#pragma unroll
+    for (int r = 1; r <= 14; r++) {
+        const int rho = r < 14 ? ODT_RHO[r] : ODT_RHO[13] - ODT_EPS[13], eps = r < 14 ? ODT_EPS[r] : ODT_EPS[13];
+        if (rho == 0 && eps == 0) continue;
+        const uint32_t kk[4] = {dk[4 * r], dk[4 * r + 1], dk[4 * r + 2], dk[4 * r + 3]};
+#pragma unroll
+        for (int j = 0; j < 4; j++) dk[4 * r + j] = perm(kk[j], kk[(j + rho) & 3], sk[eps]);
+    }
+}
+DEVI void aes256_decrypt_split(const uint32_t *dk, const uint32_t in[4], uint32_t out[4], uint32_t base) {
+    uint32_t s[4] = {in[0] ^ dk[0], in[1] ^ dk[1], in[2] ^ dk[2], in[3] ^ dk[3]};
+#pragma unroll
+    for (int r = 1; r < 14; r++) odt_round_asm(s[0], s[1], s[2], s[3], base, dk[4 * r], dk[4 * r + 1], dk[4 * r + 2], dk[4 * r + 3]);
+    /* last round: byte p of word j <- Si[byte p of s_(j-3+p)]; B's word j then holds ror(out[j + 1], 8) */
+    uint32_t acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        acc[j] = ((odt_si<3>(s[j]) << 24) | (odt_si<2>(s[(j + 3) & 3]) << 16) | (odt_si<1>(s[(j + 2) & 3]) << 8) |
+                  odt_si<0>(s[(j + 1) & 3])) ^ dk[56 + j];
+    const uint32_t selr = (base & 0x40u) ? 0x02010003u : 0x07060504u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) out[j] = perm(acc[j], acc[(j + 3) & 3], selr);
+}
+#endif
+
 #define ODT_CHECK_THREADS 512
 __global__ void __launch_bounds__(ODT_CHECK_THREADS, 4)   /* 2 workgroups (64 KiB table each) per CU */
 k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
@@ -365,10 +448,18 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     __shared__ uint32_t flag;
     for (uint32_t k = threadIdx.x; k < 256u * ODT_TD_ROW / 4; k += blockDim.x) {
         const uint32_t x = k >> 6, c = k & 63u;
-        odt_td[k] = c < 32u ? T->td0[x] : (uint32_t)T->inv_sbox[x];
+        if (ODT_SPLIT) odt_td[k] = ror32(T->td0[x], 8u * (c >> 4));               /* Td_(c/16), copy c % 16 */
+        else odt_td[k] = c < 32u ? T->td0[x] : (uint32_t)T->inv_sbox[x];
+    }
+    if (ODT_SPLIT && threadIdx.x < 64u) {
+        const uint32_t x = 4u * threadIdx.x;                                     /* the Si row at 0x10000 */
+        odt_td[256u * ODT_TD_ROW / 4 + threadIdx.x] = (uint32_t)T->inv_sbox[x] | ((uint32_t)T->inv_sbox[x + 1] << 8) |
+                                                     ((uint32_t)T->inv_sbox[x + 2] << 16) | ((uint32_t)T->inv_sbox[x + 3] << 24);
     }
     if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
-    const uint32_t lanec = (threadIdx.x & 31u) << 2;
+    const uint32_t lanec = (threadIdx.x & (ODT_SPLIT ? 15u : 31u)) << 2;
+    /* split tables: byte t = row offset of the copy lookup t reads (A: Td_t, B: Td_t+1) */
+    const uint32_t base = lanec * 0x01010101u + ((threadIdx.x & 16u) ? 0x00c08040u : 0xc0804000u);
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = g < e.count;
     uint32_t key[8];
@@ -378,11 +469,17 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     uint32_t rk[60], dk[60];
     aes256_expand(L, key, rk);
     aes_dec_schedule<14>(L, rk, dk);
+#if ODT_SPLIT
+    odt_dk_split(dk, base);
+#define ODT_DECRYPT(dk, ct, pt) aes256_decrypt_split(dk, ct, pt, base)
+#else
+#define ODT_DECRYPT(dk, ct, pt) aes256_decrypt_rep(dk, ct, pt, lanec)
+#endif
     bool ok;
     if (p.enc_len == 16u) {
         /* experimental 2-byte check (:98-101) */
         uint32_t ct[4] = {p.enc[0], p.enc[1], p.enc[2], p.enc[3]}, pt[4];
-        aes256_decrypt_rep(dk, ct, pt, lanec);
+        ODT_DECRYPT(dk, ct, pt);
         ok = ((pt[0] ^ p.iv[0]) >> 16) == 0x0300u;
     } else {
         /* SHA256 over the first min(len,1024) plaintext bytes == checksum (:104-123) */
@@ -396,7 +493,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
             for (int q = 0; q < 4; q++) {
                 const uint32_t *cp = p.enc + (b * 4u + q) * 4u;
                 uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
-                aes256_decrypt_rep(dk, ct, pt, lanec);
+                ODT_DECRYPT(dk, ct, pt);
 #pragma unroll
                 for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
             }
@@ -409,7 +506,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
             if ((uint32_t)q < (rem >> 4)) {
                 const uint32_t *cp = p.enc + (nfull * 4u + q) * 4u;
                 uint32_t ct[4] = {cp[0], cp[1], cp[2], cp[3]}, pt[4];
-                aes256_decrypt_rep(dk, ct, pt, lanec);
+                ODT_DECRYPT(dk, ct, pt);
 #pragma unroll
                 for (int k = 0; k < 4; k++) { w[4 * q + k] = pt[k] ^ prev[k]; prev[k] = ct[k]; }
             } else {
@@ -428,6 +525,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
         for (int k = 0; k < 8; k++) ok = ok && st[k] == p.checksum[k];
     }
     if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+#undef ODT_DECRYPT
 }
 #endif /* DPRF_PART_ODT */
 
