@@ -458,7 +458,9 @@ DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8
 
 /* Write K[0:bs] (BE words) at byte `len` of the slot's period and repeat the period's first 16 bytes
  * after it (a 16-byte block read starting at o < Lp then never wraps). */
-DEVI void r6_store_k(const r6_lds &S, uint32_t len, uint32_t bs, const uint32_t K[16]) {
+/* colbytes: the column's size in bytes -- the wrap copy stops there (range mode sizes the column to the bytes its
+ * block reads can reach, launch_pdf_r6) */
+DEVI void r6_store_k(const r6_lds &S, uint32_t len, uint32_t bs, const uint32_t K[16], uint32_t colbytes) {
 #pragma unroll
     for (int k = 0; k < 64; k++) {
         if ((uint32_t)k < bs) {
@@ -467,7 +469,8 @@ DEVI void r6_store_k(const r6_lds &S, uint32_t len, uint32_t bs, const uint32_t 
         }
     }
     const uint32_t Lp = len + bs;
-    for (uint32_t k = 0; k < 16; k++) *L8(S.pat + pat_addr(Lp + k, S.lanebase)) = *L8(S.pat + pat_addr(k, S.lanebase));
+    for (uint32_t k = 0; k < 16 && Lp + k < colbytes; k++)
+        *L8(S.pat + pat_addr(Lp + k, S.lanebase)) = *L8(S.pat + pat_addr(k, S.lanebase));
 }
 
 /* Four BE words starting at byte o of the slot's period (one v_perm per word). */
@@ -507,7 +510,7 @@ DEVI uint32_t r6_family(const r6_lds &S, uint32_t len) {
  * every batch one family, so Lp, the block offset o and the byte selector are wave-uniform scalars and a
  * block's LDS address is one v_add of the lane's column base (~15 VALU slots per AES block saved). */
 template <bool UNI>
-DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16]) {
+DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16], uint32_t colbytes) {
     uint32_t Lp = len + bs;
     if (UNI) Lp = __builtin_amdgcn_readfirstlane(Lp);
     const uint32_t colbase = S.pat + S.lanebase;                 /* pat is only 16-byte aligned */
@@ -536,7 +539,10 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
                 const lds_u32 *col = L32(colbase + ((o >> 2) << 8));
                 uint32_t lw[5];
 #pragma unroll
-                for (int k = 0; k < 5; k++) lw[k] = col[k * 64];
+                for (int k = 0; k < 4; k++) lw[k] = col[k * 64];
+                /* the fifth word only for a block that does not start on a word (o is uniform: a scalar branch);
+                 * the column ends where the aligned blocks' reads do (launch_pdf_r6) */
+                lw[4] = (o & 3u) ? col[4 * 64] : lw[3];
 #pragma unroll
                 for (int k = 0; k < 4; k++) v[k] = perm(lw[k + 1], lw[k], sel);
             } else {
@@ -584,7 +590,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #pragma unroll
     for (int k = 0; k < 16; k++) K[k] = hs[k];
     bs = 32u + 16u * hsel;
-    r6_store_k(S, len, bs, K);
+    r6_store_k(S, len, bs, K, colbytes);
     return prev[3] & 0xffu;
 }
 
@@ -618,7 +624,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #define R6_LANES 768
 #endif
 #ifndef R6_MAX_SLOTS
-#define R6_MAX_SLOTS 1280
+#define R6_MAX_SLOTS 1088           /* 17 groups: the slot arrays sized so that 16 groups of 21-word columns fit */
 #endif
 #define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
 #define R6_CLASSES 6
@@ -630,7 +636,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #ifndef R6_START_BATCH
 #define R6_START_BATCH 0
 #endif
-#define R6_QUEUES (R6_CLASSES + 1)
+#define R6_QUEUES (R6_CLASSES + (R6_START_BATCH ? 1 : 0))
 #define R6_START_Q R6_CLASSES
 #define R6_MAP_WORDS ((R6_MAX_SLOTS + 31) / 32)
 #define R6_IDLE 0xffffffffu
@@ -642,7 +648,7 @@ struct r6_shared {
     uint32_t map[R6_QUEUES][R6_MAP_WORDS];    /* queued slots of each class (+ the start queue), a bit per slot */
     uint32_t count[R6_QUEUES];                /* queued slots per queue (a hint for picking one)       */
     uint32_t live;                            /* slots holding a candidate                             */
-    uint32_t nslots, te_slots, ncand;
+    uint32_t nslots, te_slots, ncand, pat_words;
     const uint32_t *slots;                    /* e.slots, e.lens (list mode), likewise */
     const uint8_t *lens;
     unsigned long long start;                 /* e.start / e.count (ncand) read from here when a slot takes or reports a
@@ -722,7 +728,7 @@ DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
     if (c == R6_IDLE) return false;
     uint32_t K[16];
     const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, lds_load64(&sh->start) + c, c, sh->slots, sh->lens, S, K);
-    r6_store_k(S, len, 32u, K);
+    r6_store_k(S, len, 32u, K, MODE == 0 ? 4u * lds_load(&sh->pat_words) : ~0u);   /* list mode: full wrap */
     sh->state[slot] = len | (32u << 8);
     return true;
 }
@@ -828,6 +834,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         sh->live = 0u;
         sh->start = e.start;
         sh->ncand = e.count;
+        sh->pat_words = pat_words;
         sh->slots = e.slots;
         sh->lens = e.lens;
     }
@@ -888,7 +895,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             const uint32_t len = st & 0xffu, hs = st >> 30;
             uint32_t bs = (st >> 8) & 0xffu, i = (st >> 16) & 0x3fffu;
             uint32_t K[16];
-            const uint32_t last = r6_round<MODE == 0>(S, len, bs, hs, K);
+            const uint32_t last = r6_round<MODE == 0>(S, len, bs, hs, K, MODE == 0 ? 4u * lds_load(&sh->pat_words) : ~0u);
             i++;
             bool more = true;
             if (i >= 64u && i >= last + 32u) {                    /* loop condition of :247 */
@@ -929,6 +936,8 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
 
 /* Slot capacity of one workgroup: 32-slot groups in the upper halves of the Te0 rows, then 64-slot groups
  * in the dynamic LDS left next to the table and the shared block (160 KiB per workgroup). */
+/* -pr 6 (21-word columns, r6_pat_words): 16 groups of 64 slots beside the tables and the shared block */
+static_assert(R6_TE_BYTES + 256 + (sizeof(r6_shared) + 15) / 16 * 16 + 16 * 21 * 256 <= 160 * 1024, "16 groups at -pr 6");
 static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots, size_t *shm) {
     const size_t fixed = R6_TE_BYTES + 256 + (sizeof(r6_shared) + 15) / 16 * 16;
     const uint32_t te_groups = R6_TE_USED <= 128 ? 256u / pat_words : 0u;
@@ -941,6 +950,26 @@ static void r6_capacity(uint32_t pat_words, uint32_t *nslots, uint32_t *te_slots
     *shm = 256 + (sizeof(r6_shared) + 15) / 16 * 16 + (size_t)(dyn / 64u) * pat_words * 256u;   /* + static r6_te */
 }
 
+/* Words per period column.  List mode: the period (lmax + 64) + 16 wrap bytes and the fifth word of any block read
+ * (r6_read16 takes 5 words from word o / 4).  Range mode: exactly the words the reads reach -- the block of a round
+ * starts at o = 16 q mod Lp (Lp = lmax + bs, so o runs over the multiples of gcd(16, Lp)) and takes 4 words, 5 when
+ * o is not a word start; r6_load_k reads 5 words from bytes lmax and lmax + 16.  Even password lengths then need one
+ * word less (21 instead of 22 at -pr 6: 1,024 slots per CU instead of 960). */
+static uint32_t r6_pat_words(uint32_t mode, uint32_t lmax) {
+    if (mode != 0) return ((lmax + 63u) >> 2) + 5u;
+    uint32_t mx = ((lmax + 16u) >> 2) + 5u;
+    for (uint32_t bs = 32; bs <= 64; bs += 16) {
+        const uint32_t Lp = lmax + bs;
+        uint32_t g = 16;
+        while (Lp % g) g >>= 1;
+        for (uint32_t o = 0; o < Lp; o += g) {
+            const uint32_t w = (o >> 2) + ((o & 3u) ? 5u : 4u);
+            if (w > mx) mx = w;
+        }
+    }
+    return mx;
+}
+
 #define R6_MAX_DEVICES 64
 static std::mutex r6_attr_mu;
 static bool r6_attr_set[2][R6_MAX_DEVICES];
@@ -950,9 +979,7 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     /* longest password of the launch (list mode: the host's maximum over the chunk): the period length
      * and with it the slots per CU follow the actual candidates, not the 64-byte slot width */
     const uint32_t lmax = e.pwlen < 4u * DPRF_SLOT_WORDS ? e.pwlen : 4u * DPRF_SLOT_WORDS;
-    /* period (lmax + 64) + 16 wrap bytes: a block read starts at byte o < lmax + 64 and takes the 5 words
-     * from word o / 4 (the wrap bytes end inside them) */
-    const uint32_t pat_words = ((lmax + 63u) >> 2) + 5u;
+    const uint32_t pat_words = r6_pat_words(e.mode, lmax);
     uint32_t nslots = 0, te_slots = 0;
     size_t shm = 0;
     r6_capacity(pat_words, &nslots, &te_slots, &shm);
