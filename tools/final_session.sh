@@ -24,4 +24,12 @@ cp profiles/pmc_traffic.json profiles/pmc_valu.json gpurun_out/
 echo "== bench $(date +%T)"
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench_$TAG.json')); r=d['roofline']; print(d['value'], r['frac'], r['bound'], r['rocprof']['stale'], r['traffic_source']['stale'], {k: (round(v['value']/1e6,3), v.get('rocprof',{}).get('stale')) for k, v in d['per_format'].items()})"
+if [ -n "$REHEARSE" ]; then
+  # the N>1 paths on the one-GPU box, same build: the library's multi-device path (two device lanes on device 0) and
+  # the driver's torchrun path (two ranks on device 0, gloo for the exchanges RCCL refuses on one GPU)
+  echo "== rehearsals $(date +%T)"
+  DPRF_BENCH_SAME_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --no-side --cpu-seconds 0 --steps 3 > gpurun_out/bench_lanes2_$TAG.json 2> gpurun_out/bench_lanes2_$TAG.err || { tail -20 gpurun_out/bench_lanes2_$TAG.err; exit 1; }
+  DPRF_BENCH_SAME_DEVICE=1 DPRF_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_n2_rehearsal_$TAG.json 2> gpurun_out/bench_n2_rehearsal_$TAG.err || { tail -20 gpurun_out/bench_n2_rehearsal_$TAG.err; exit 1; }
+  python -c "import json; [print(f, json.loads(open('gpurun_out/'+f).read().strip().splitlines()[-1])['value']) for f in ('bench_lanes2_$TAG.json', 'bench_n2_rehearsal_$TAG.json')]"
+fi
 echo "== done $(date +%T)"
