@@ -457,6 +457,12 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
                                                      ((uint32_t)T->inv_sbox[x + 2] << 16) | ((uint32_t)T->inv_sbox[x + 3] << 24);
     }
     if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
+    /* odt_round_asm uses the v_perm result as the whole LDS address: the table must sit at LDS address 0 (checked;
+     * a build that ever breaks this fails loudly instead of computing wrong) */
+    if (ODT_SPLIT && (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)odt_td != 0u) {
+        if (threadIdx.x == 0) atomicOr(&R->pad_, 4u);
+        return;
+    }
     const uint32_t lanec = (threadIdx.x & (ODT_SPLIT ? 15u : 31u)) << 2;
     /* split tables: byte t = row offset of the copy lookup t reads (A: Td_t, B: Td_t+1) */
     const uint32_t base = lanec * 0x01010101u + ((threadIdx.x & 16u) ? 0x00c08040u : 0xc0804000u);

@@ -757,10 +757,12 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
         const uint32_t v = __builtin_amdgcn_readlane(cnt, c);
         if (v > bc) { bc = v; best = c; }
     }
-    if (R6_START_BATCH) {
+#if R6_START_BATCH
+    {
         const uint32_t vs = __builtin_amdgcn_readlane(cnt, R6_START_Q);
         if (vs >= R6_START_BATCH || (bc == 0 && vs > 0)) { bc = vs; best = R6_START_Q; }
     }
+#endif
     *queue = best;
     if (bc == 0) return 0;
     const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
@@ -819,6 +821,12 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     r6_shared *sh = (r6_shared *)((uint8_t *)smem + 256);
     const uint32_t patbase = lds_addr(smem) + 256u + (uint32_t)((sizeof(r6_shared) + 15) / 16 * 16);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nthr = blockDim.x;
+    /* the asm rounds use the v_perm result as the whole LDS address: r6_te must sit at LDS address 0 (it is this
+     * kernel's only static LDS object).  A build that ever breaks this fails loudly instead of computing wrong. */
+    if (lds_addr(r6_te) != 0u) {
+        if (tid == 0) atomicOr(&R->pad_, 8u);
+        return;
+    }
     /* the tables' copies fill the first R6_TE_USED bytes of each row: table t = ror(Te0, 8t) (16t with two
      * tables); the rest of a row, if any, holds slot periods */
     constexpr uint32_t TW = R6_TE_USED / 4;                                     /* table words per row */
@@ -876,7 +884,8 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         t_nb++;
         t_part += n;
 #endif
-        if (R6_START_BATCH && queue == R6_START_Q) {
+#if R6_START_BATCH
+        if (queue == R6_START_Q) {
             /* a batch of slots whose candidates finished: they take their next candidates together (one cursor
              * atomic for the wave), start them and queue their first rounds, or retire when the cursor is dry */
             if (slot != R6_IDLE) {
@@ -889,6 +898,9 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
             R6T_MARK(t_work)
             continue;
         }
+#else
+        (void)queue;
+#endif
         if (slot != R6_IDLE) {
             const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
             const uint32_t st = sh->state[slot];
@@ -909,17 +921,17 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     atomicMin(&R->first, idx);
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
-                if (R6_START_BATCH) {
-                    /* to the start queue (the slot stays live until it takes a candidate or retires) */
-                    more = false;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    atomicOr(&sh->map[R6_START_Q][slot >> 5], 1u << (slot & 31u));
-                    atomicAdd(&sh->count[R6_START_Q], 1u);
-                } else {
-                    /* the finishing lanes of the batch take their next candidates together */
-                    more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
-                    if (!more) atomicSub(&sh->live, 1u);
-                }
+#if R6_START_BATCH
+                /* to the start queue (the slot stays live until it takes a candidate or retires) */
+                more = false;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                atomicOr(&sh->map[R6_START_Q][slot >> 5], 1u << (slot & 31u));
+                atomicAdd(&sh->count[R6_START_Q], 1u);
+#else
+                /* the finishing lanes of the batch take their next candidates together */
+                more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
+                if (!more) atomicSub(&sh->live, 1u);
+#endif
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);
             }

@@ -31,7 +31,9 @@ struct dprf_results {
     uint32_t nhits;                 /* total hits (may exceed cap) */
     uint32_t stop;                  /* set by a hit when stop_on_first */
     uint32_t cursor;                /* work cursor of persistent kernels (PDF R6), reset per launch */
-    uint32_t pad_;                  /* error flags set by a kernel (PDF R6 scheduler watchdog), 0 = none */
+    uint32_t pad_;                  /* error flags set by a kernel, 0 = none: 1 PDF R6 scheduler watchdog, 2 / 4 / 8 an
+                                       asm block's LDS-address assumption broken (R2-R4 S-box area, ODF check table,
+                                       R6 tables) */
     unsigned long long first;       /* lowest hit index (atomicMin), ~0 if none */
     unsigned long long skipped;     /* candidates of launched chunks NOT evaluated: stop_on_first blocks
                                        skipped above the lowest hit (rare: one atomic per skipped block, none
