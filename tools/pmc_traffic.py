@@ -43,6 +43,7 @@ for w, kname in DOM.items():
                        "lds_busy": v.get("lds_busy"), "lds_util": v.get("lds_util"),
                        "effective_clock_GHz": v.get("effective_clock_GHz"),
                        "valu_active_per_wave_cycle": v.get("valu_active_per_wave_cycle"),
+                       "wait_any_frac": v.get("wait_any_frac"), "wait_inst_any_frac": v.get("wait_inst_any_frac"),
                        "SQ_LDS_BANK_CONFLICT_per_launch": pd.get("SQ_LDS_BANK_CONFLICT"),
                        # bank-conflict cycles (summed over the CUs) per CU cycle of the dispatch
                        "lds_bank_conflict_frac": (pd["SQ_LDS_BANK_CONFLICT"] / (CUS * pd["GRBM_GUI_ACTIVE"] / XCDS)
