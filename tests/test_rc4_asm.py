@@ -199,7 +199,7 @@ def test_generated_ksa_equals_rc4(nk):
 
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr"])
+                                  "--jctr", "--early-v1"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""

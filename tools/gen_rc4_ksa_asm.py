@@ -42,6 +42,8 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     group and repaired for its S[j] stores)
        tools/gen_rc4_ksa_asm.py --salu-consts > <variant header>  (A/B, round-3 first version: compare constants
                                                                     through two s_movk per group)
+       tools/gen_rc4_ksa_asm.py --early-v1 > <variant header>     (A/B: step 1's compare-select and j add hoisted
+                                                                    above step 0's LDS pair, same instructions)
        tools/gen_rc4_ksa_asm.py --jctr > <variant header>         (A/B: i0 / i1 counted in byte 3 of j, key registers
                                                                     carrying the counter steps: 603 vs 612 M, slower)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
@@ -175,6 +177,63 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
     return out
 
 
+def ksa_early_v1(nk):
+    """vconst schedule with step 1's dependencies hoisted above step 0's LDS pair: the hit1 compare right after the
+    j add, then the S[j0] address, v1 and the step-1 j add, and only then x0 = S[j0] / S[j0] = W.b0 -- the chain
+    j0 -> v1 -> j1 -> S[j1] address no longer waits behind two LDS instructions (same instruction count)."""
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, IA, C16, D0 = (
+        "%%%d" % k for k in range(21))
+    KB = ["%%%d" % (21 + k) for k in range(nk)]
+    out = []
+    e = out.append
+    identity(e, M, M0S, SB)
+    e("v_mov_b32 %s, 0" % J)
+    e("v_mov_b32 %s, 0x100" % W)
+    IC = WN
+    FIRST_IC = 32
+    e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
+
+    def cmp(i, sel):
+        if q < FIRST_IC:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i))
+        else:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:%s" % (J, IC, sel))
+
+    for q in range(128):
+        i0, i1 = 2 * q, 2 * q + 1
+        if q > 0:
+            e("s_waitcnt lgkmcnt(1)")
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
+        cmp(i1, "BYTE_1")
+        e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A0, J))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
+          % (V1, W, W))
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
+        e("ds_read_u8 %s, %s" % (X0, A0))
+        e("ds_write_b8 %s, %s" % (A0, W))
+        e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A1, J))
+        cmp(i0, "BYTE_0")
+        e("ds_read_u8 %s, %s" % (X1, A1))
+        e("ds_write_b8 %s, %s" % (A1, V1))
+        if FIRST_IC <= q < 127:
+            e("v_add_u32 %s, 0x202, %s" % (IC, IC))
+        if q < 127:
+            e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
+            e("s_waitcnt lgkmcnt(1)")
+        else:
+            e("s_waitcnt lgkmcnt(0)")
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+          % (M, X1, X0))
+        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(2 * q)))
+    e("s_waitcnt lgkmcnt(0)")
+    return out
+
+
 def identity(e, M, M0S, SB):
     e("s_mov_b32 %s, m0" % M0S)
     e("s_mov_b32 m0, %s" % SB)
@@ -291,7 +350,8 @@ def main():
     print("#define RC4_KSA_KB_CTR %d" % (1 if jctr else 0))
     print("#define RC4_KSA_NKR_5 %d" % nkr_of(5, jctr))
     for nk in KEYLENS:
-        lines = ksa(nk, early, late, pre, vconst and not early, b128, jctr)
+        lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
