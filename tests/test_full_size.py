@@ -27,6 +27,10 @@ CASES = [
     ("configs2-pdf-r4-alnum7", "pdf", {"R": 4, "length": 128}, ALNUM, "q7ZpL02", 1 << 24),
     ("configs2-pdf-r3-alnum7-last", "pdf", {"R": 3, "length": 128}, ALNUM, "9999999", 1 << 24),
     ("configs3-pdf-r6-lower6", "pdf", {"R": 6, "length": 256}, LOWER, "zyxwvu", 1 << 19),
+    # R6 at the other column shapes of range mode (dprf_kernels_r6.hip r6_pat_words): odd length (blocks at odd
+    # offsets, the fifth word and a partial wrap) and a multiple of 4 (every block word-aligned, 20-word columns)
+    ("pdf-r6-lower7", "pdf", {"R": 6, "length": 256}, LOWER, "qnbvcxz", 1 << 17),
+    ("pdf-r6-lower8", "pdf", {"R": 6, "length": 256}, LOWER, "plokijuh", 1 << 17),
     ("pdf-r2-alnum7", "pdf", {"R": 2, "length": 40}, ALNUM, "Mo3kV9b", 1 << 26),
     ("pdf-r5-alnum7-first", "pdf", {"R": 5, "length": 256}, ALNUM, "aaaaaaa", 1 << 26),
 ]
@@ -43,6 +47,8 @@ TWO_WAY = [
     ("configs0-office-pr8", "docx", {}, LOWER, "pwzqxkmv", 1 << 13),
     ("configs1-odt-alnum6", "odt", {}, ALNUM, "Zx9Qa7", 1 << 17),
     ("configs3-pdf-r6-lower6", "pdf", {"R": 6, "length": 256}, LOWER, "zyxwvu", 1 << 14),
+    ("pdf-r6-lower7", "pdf", {"R": 6, "length": 256}, LOWER, "qnbvcxz", 1 << 12),
+    ("pdf-r6-lower8", "pdf", {"R": 6, "length": 256}, LOWER, "plokijuh", 1 << 12),
 ]
 ORACLE_THREADS = 16      # the GPU box's CPU share
 
