@@ -74,6 +74,56 @@ DEVI void sha1_compress(uint32_t st[5], uint32_t w[16]) {
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
 }
+/* SHA-1 from a fixed starting state (PBKDF2's HMAC midstates: the same for all 1,023 iterations of a candidate).
+ * sha1_pre computes, once per candidate, everything of rounds 0-4 that does not depend on the message: round 0's
+ * whole sum but w0, round 1's f + e + k as ONE value (LLVM hoists f and e + k as two), and e + k of rounds 2-4.  They
+ * leave through an empty asm so that LLVM cannot re-split them inside the loop.  2,070 -> 2,062 issue slots per
+ * PBKDF2 iteration (tools/asm_slots.py); the extra live values need more than the 64 VGPRs of 8 waves per SIMD
+ * (k_odt_kdf runs at ODT_KDF_WAVES). */
+struct sha1_pre_t { uint32_t p0, p1, p2, p3, p4, ra, rb; };
+DEVI sha1_pre_t sha1_pre(const uint32_t st[5]) {
+    const uint32_t K = 0x5A827999u, A = st[0], B = st[1], C = st[2], D = st[3], E = st[4];
+    sha1_pre_t P;
+    P.ra = rol32(A, 30);
+    P.rb = rol32(B, 30);
+    P.p0 = rol32(A, 5) + f_ch(B, C, D) + E + K;
+    P.p1 = f_ch(A, P.rb, C) + D + K;
+    P.p2 = C + K;
+    P.p3 = P.rb + K;
+    P.p4 = P.ra + K;
+    asm volatile("" : "+v"(P.p0), "+v"(P.p1), "+v"(P.p2), "+v"(P.p3), "+v"(P.p4));
+    return P;
+}
+/* st: the fixed starting state, out = st + the compression of w (w is overwritten by the schedule) */
+DEVI void sha1_compress_pre(const uint32_t st[5], const sha1_pre_t &P, uint32_t w[16], uint32_t out[5]) {
+    const uint32_t K = 0x5A827999u;
+    const uint32_t a1 = P.p0 + w[0];
+    const uint32_t a2 = rol32(a1, 5) + P.p1 + w[1];
+    const uint32_t a3 = rol32(a2, 5) + f_ch(a1, P.ra, P.rb) + P.p2 + w[2];
+    const uint32_t r1 = rol32(a1, 30);
+    const uint32_t a4 = rol32(a3, 5) + f_ch(a2, r1, P.ra) + P.p3 + w[3];
+    const uint32_t r2 = rol32(a2, 30);
+    const uint32_t a5 = rol32(a4, 5) + f_ch(a3, r2, r1) + P.p4 + w[4];
+    uint32_t a = a5, b = a4, c = rol32(a3, 30), d = r2, e = r1;
+#pragma unroll
+    for (int t = 5; t < 80; t++) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rol32(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        uint32_t f, k;
+        if (t < 20)      { f = f_ch(b, c, d);  k = K; }
+        else if (t < 40) { f = xor3(b, c, d);  k = 0x6ED9EBA1u; }
+        else if (t < 60) { f = f_maj(b, c, d); k = 0x8F1BBCDCu; }
+        else             { f = xor3(b, c, d);  k = 0xCA62C1D6u; }
+        const uint32_t tmp = rol32(a, 5) + f + e + (k + wt);
+        e = d; d = c; c = rol32(b, 30); b = a; a = tmp;
+    }
+    out[0] = st[0] + a; out[1] = st[1] + b; out[2] = st[2] + c; out[3] = st[3] + d; out[4] = st[4] + e;
+}
 DEVI void sha1_iv(uint32_t st[5]) {
     st[0] = SHA1_IV0; st[1] = SHA1_IV1; st[2] = SHA1_IV2; st[3] = SHA1_IV3; st[4] = SHA1_IV4;
 }

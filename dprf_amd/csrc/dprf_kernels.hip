@@ -256,8 +256,11 @@ k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf
 /* ================================================================== ODF 1.2 (AES-256-CBC, PBKDF2-HMAC-SHA1) */
 /* Two launches per batch, as for Office: k_odt_kdf (SHA-256 start key + PBKDF2, 8 waves/SIMD) leaves the
  * 32-byte AES-256 key of every candidate in HBM; k_odt_check decrypts and verifies. */
+#ifndef ODT_KDF_WAVES
+#define ODT_KDF_WAVES 6             /* waves per SIMD: 8 / 6 / 4 measured the same (round 2); 6 leaves room for sha1_pre */
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(256, 8)
+__global__ void __launch_bounds__(256, ODT_KDF_WAVES)
 k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
@@ -286,34 +289,38 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
         for (int j = 0; j < 16; j++) w[j] = 0x5c5c5c5cu ^ (j < 8 ? sk[j] : 0u);
         sha1_iv(ost); sha1_compress(ost, w);
     }
-    uint32_t key[8];
+    /* the midstates' message-independent parts of rounds 0-4, once per candidate (dev_crypto.h sha1_pre) */
+    const sha1_pre_t ipre = sha1_pre(ist), opre = sha1_pre(ost);
 #pragma unroll
     for (int blkno = 1; blkno <= 2; blkno++) {
         uint32_t u[5], t[5];
         {
             uint32_t w[16] = {p.salt[0], p.salt[1], p.salt[2], p.salt[3], (uint32_t)blkno, 0x80000000u,
                               0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
-            uint32_t s[5] = {ist[0], ist[1], ist[2], ist[3], ist[4]};
-            sha1_compress(s, w);
+            uint32_t s[5];
+            sha1_compress_pre(ist, ipre, w, s);
             uint32_t w2[16] = {s[0], s[1], s[2], s[3], s[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
-            u[0] = ost[0]; u[1] = ost[1]; u[2] = ost[2]; u[3] = ost[3]; u[4] = ost[4];
-            sha1_compress(u, w2);
+            sha1_compress_pre(ost, opre, w2, u);
         }
         t[0] = u[0]; t[1] = u[1]; t[2] = u[2]; t[3] = u[3]; t[4] = u[4];
         for (int it = 1; it < 1024; it++) {
             uint32_t w[16] = {u[0], u[1], u[2], u[3], u[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
-            uint32_t s[5] = {ist[0], ist[1], ist[2], ist[3], ist[4]};
-            sha1_compress(s, w);
+            uint32_t s[5];
+            sha1_compress_pre(ist, ipre, w, s);
             uint32_t w2[16] = {s[0], s[1], s[2], s[3], s[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
-            u[0] = ost[0]; u[1] = ost[1]; u[2] = ost[2]; u[3] = ost[3]; u[4] = ost[4];
-            sha1_compress(u, w2);
+            sha1_compress_pre(ost, opre, w2, u);
             t[0] ^= u[0]; t[1] ^= u[1]; t[2] ^= u[2]; t[3] ^= u[3]; t[4] ^= u[4];
         }
-        if (blkno == 1) { key[0] = t[0]; key[1] = t[1]; key[2] = t[2]; key[3] = t[3]; key[4] = t[4]; }
-        else { key[5] = t[0]; key[6] = t[1]; key[7] = t[2]; }
-    }
+        /* each block's key words go out as soon as they are known (block 1's five need not stay live through
+         * block 2) */
+        if (blkno == 1) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) keys[(size_t)k * e.count + g] = key[k];
+            for (int k = 0; k < 5; k++) keys[(size_t)k * e.count + g] = t[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) keys[(size_t)(5 + k) * e.count + g] = t[k];
+        }
+    }
 }
 
 /* The 64 AES-256 block decryptions per candidate read Td0 14,336 times.  A single 1 KiB Td0 puts
