@@ -1,6 +1,8 @@
 """GPU parity: libdprf.so's kernels vs the reference's verdicts (golden fixtures) and vs the oracle, through
 the C ABI.  Bit-exact: hit sets must be identical."""
 import random
+import tempfile
+import zlib
 
 import pytest
 
@@ -98,12 +100,48 @@ def _random_words(rng, n, lo=1, hi=12, alphabet=ALNUM):
                                     ("pdf_synth_r6_ox", 150), ("odt_testdoc_e", 800), ("odt_testdoc_std", 400),
                                     ("office_testdoc", 24)])
 def test_random_lists_vs_oracle(dprf, oracle, streams, name, n):
-    rng = random.Random(hash(name) & 0xffff)
+    rng = random.Random(zlib.crc32(name.encode()))      # str hash() is salted per process
     words = _random_words(rng, n) + [streams[name]["password"]]
     rng.shuffle(words)
     want = [i for i, v in enumerate(oracle.Ctx(streams[name]["stream"]).verify_list(words)) if v == 1]
     hits, _, _ = ctx_for(dprf, streams, name).verify_list(words)
     assert hits == want
+
+
+# (writer kind, writer kwargs, candidates per document): every revision / key length / metadata flag the
+# reference's verifiers accept (pdf_password_verifier.c:89-101), both ODF streams, Office
+RANDOM_DOCS = [
+    ("pdf", {"R": 2, "length": 40}, 2000), ("pdf", {"R": 3, "length": 128}, 2000),
+    ("pdf", {"R": 3, "length": 40}, 2000), ("pdf", {"R": 4, "length": 128, "meta": False}, 2000),
+    ("pdf", {"R": 4, "length": 128, "P": -4}, 2000), ("pdf", {"R": 5, "length": 256}, 2000),
+    ("pdf", {"R": 6, "length": 256}, 120), ("odt", {}, 300), ("odt_e", {}, 600), ("docx", {}, 12),
+]
+
+
+def _near_misses(pw):
+    """Candidates one edit away from the password (and the password itself)."""
+    flip = chr(ord(pw[-1]) ^ 1)
+    return [pw, pw[:-1], pw + "a", pw[:-1] + flip, pw.upper() if pw != pw.upper() else pw.lower(), "x" + pw]
+
+
+@pytest.mark.parametrize("seed", [101, 202, 303])
+@pytest.mark.parametrize("kind,kw,n", RANDOM_DOCS, ids=["%s%s" % (k, "".join("-%s%s" % i for i in sorted(w.items())))
+                                                       for k, w, _ in RANDOM_DOCS])
+def test_random_documents_vs_oracle(dprf, oracle, kind, kw, n, seed):
+    """Fresh documents (tests/docgen.py: random salts, IVs, IDs, O values and passwords for each seed) through
+    the parsers, then a random candidate list with the password and its near misses: GPU hit set == oracle's."""
+    from test_full_size import _doc_streams, _fields
+    rng = random.Random(seed * 1000 + zlib.crc32(repr((kind, sorted(kw.items()))).encode()))
+    pw = "".join(rng.choice(ALNUM) for _ in range(rng.randint(3, 9)))
+    with tempfile.TemporaryDirectory() as t:
+        stream = _doc_streams(t, kind, kw, pw, seed)[0]
+    words = _random_words(rng, n) + _near_misses(pw)
+    rng.shuffle(words)
+    want = [i for i, v in enumerate(oracle.Ctx(stream).verify_list(words)) if v == 1]
+    assert words.index(pw) in want
+    hits, _, st = dprf.Context(_fields(stream)).verify_list(words)
+    assert hits == want
+    assert st["candidates"] == len(words)
 
 
 @pytest.mark.parametrize("name", ["pdf_synth_r2_key", "pdf_synth_r3_l128_abc", "pdf_synth_r5_cat", "pdf_synth_r6_ox",
