@@ -42,11 +42,20 @@ WORKLOADS = {
     "pdf_r2": ("pdf_testdoc_r2", ALNUM, 7, 1 << 30, "pdf_r2", "PDF 1.3 V1/R2 (password_1.3_v1_r2.pdf), -pr 7 alnum"),
     "pdf_r5": ("pdf_synth_r5_cat", ALNUM, 7, 1 << 31, "pdf_r5", "PDF R5 (synthetic document), -pr 7 alnum"),
     "odt_e": ("odt_testdoc_e", ALNUM, 6, 1 << 24, "odt_e", "ODF -e 2-byte stream (brute_force.py:239 path), -pr 6 alnum"),
+    # configs[2] names "PDF 1.4 R3/R4": the V2/R3 128-bit path (synthetic 1.4 document) and R3 with a 40-bit key
+    # (EVP_rc4_40, pdf...c:445-453) beside the R4 test document (round 4)
+    "pdf_r3": ("pdf_synth_r3_l128_abc", ALNUM, 7, 1 << 28, "pdf_r34",
+               "configs[2]: PDF 1.4 V2/R3 128-bit key (synthetic document), -pr 7 alnum"),
+    "pdf_r3_40": ("pdf_synth_r3_l40_cab", ALNUM, 7, 1 << 28, "pdf_r3_40",
+                  "configs[2]: PDF 1.4 V2/R3 40-bit key (synthetic document), -pr 7 alnum"),
 }
 # rocprofv3 name of the dominant kernel per libdprf kernel family (the one "roofline" times)
 DOMINANT = {"office_std": "k_office_kdf", "odf_aes256": "k_odt_kdf", "pdf_r24": "k_pdf_r24", "pdf_r5": "k_pdf_r5",
             "pdf_r6": "k_pdf_r6"}
-SIDE_FORMATS = ["office", "odt_e", "pdf_r34", "pdf_r6", "pdf_r2", "pdf_r5"]
+SIDE_FORMATS = ["office", "odt_e", "pdf_r34", "pdf_r3", "pdf_r3_40", "pdf_r6", "pdf_r2", "pdf_r5"]
+# keys of a rocprof record kept in the bench line (the whole record goes to the stderr detail line)
+ROCPROF_KEYS = ("valu_busy", "valu_utilization", "lds_util", "wait_any_frac", "lds_bank_conflict_frac",
+                "effective_clock_GHz", "source", "build", "stale")
 
 
 def streams():
@@ -288,6 +297,23 @@ def measured_bound(counters, wkey):
     return work.BOUND.get(wkey, "valu"), "model"
 
 
+def compact_rocprof(rec):
+    return None if not rec else {k: rec[k] for k in ROCPROF_KEYS if rec.get(k) is not None}
+
+
+def compact_cpu(c):
+    """A CPU baseline as the bench line carries it: the figures, one short sample description (the full records,
+    with every leg's sample text, go to the stderr detail line)."""
+    if not c:
+        return c
+    out = {k: c[k] for k in ("value", "unit", "cores", "kind", "nproc", "cpu_share") if k in c}
+    out["sample"] = c.get("sample", "")[:160]
+    for k in ("one_worker", "process_model_4"):
+        if c.get(k):
+            out[k] = {"value": c[k]["value"], "cores": c[k]["cores"]}
+    return out
+
+
 def device_balance(ctx):
     """Per-device split of the last library call (dprf_ctx_last_call_devices) when this process drives several
     GPUs through one context: candidates, launches, finish time, and the last device's finish over the mean."""
@@ -329,6 +355,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cluster", action="store_true", help="skip the configs[4] server + GPU client leg")
     ap.add_argument("--cluster-candidates", type=int, default=12 << 20)
+    ap.add_argument("--side-steps", type=int, default=5, help="timed steps of each per-format leg (1 warmup)")
     ap.add_argument("--stop-on-first", action="store_true",
                     help="time the product's early-stop rounds instead of full verification of every batch")
     args = ap.parse_args()
@@ -424,12 +451,14 @@ def main():
             sn, scs, spl, sB, skey, sdesc = WORKLOADS[name]
             sf = quiet_fields(brute_force, S[sn]["stream"])
             sctx = _lib.Context(sf, devices=devices)
-            sdt, sst, _, spl = run_workload(name, sctx, rank, world, 2, 1, sync, allreduce_min, ndev=len(devices))
+            sdt, sst, _, spl = run_workload(name, sctx, rank, world, args.side_steps, 1, sync, allreduce_min,
+                                            ndev=len(devices))
             sdt = allreduce_max(sdt)
             sm = summarize(sst, skey, world, sdt)
             side[name] = {"value": sm["value"], "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
                           "pwlen": spl, "bound": measured_bound(pmc_summary(name, build), skey)[0],
-                          "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
+                          "steps": args.side_steps, "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
+                          "dominant_avg_ms": sm["avg_launch_ms"], "candidates_per_launch": sm["per_launch"],
                           "valu_floor_frac": (sm["per_launch"] * work.per_candidate(skey)
                                               / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak),
                           "call_overhead": sm["call_overhead"]}
@@ -438,13 +467,13 @@ def main():
                     skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
             pc = pmc_summary(name, build)
             if pc:
-                side[name]["rocprof"] = pc
+                side[name]["rocprof"] = compact_rocprof(pc)
             tr, trec = launch_traffic(pmc, name, sm["per_launch"], build)
             if tr is not None:
                 side[name]["traffic_bytes_per_launch"] = tr
                 side[name]["traffic_source"] = {k: trec.get(k) for k in ("source", "build", "stale")}
             if name in side_cpu:
-                side[name]["cpu_baseline"] = side_cpu[name]
+                side[name]["cpu_baseline"] = compact_cpu(side_cpu[name])
             sctx.close()
 
     cluster = None
@@ -480,7 +509,7 @@ def main():
         if counters:
             roof["valu_busy"] = counters.get("valu_busy")
             roof["valu_utilization"] = counters.get("valu_utilization")
-            roof["rocprof"] = counters
+            roof["rocprof"] = compact_rocprof(counters)
         out = {
             "metric": METRIC,
             "value": m["cands"] * world / dt_max,
@@ -502,13 +531,26 @@ def main():
                            n_gpus, "one process per GPU" if dist else
                            "one process, %d-device library context" % len(devices))},
             "roofline": roof,
-            "cpu_baseline": cpu,
+            "cpu_baseline": compact_cpu(cpu),
             "per_format": side,
-            "cluster": cluster,
+            "cluster": None if cluster is None else {k: v for k, v in cluster.items() if not isinstance(v, (list, dict))},
             "lowest_hit_index": None if lowest is None or lowest >= (1 << 62) else lowest,
         }
         if balance:
             out["device_balance"] = balance
+        # every workload's figure in a few hundred bytes at the END of the line, so that a log tail shows all of
+        # them (the 16 KB driver tail started inside the per-format CPU samples)
+        summ = {args.workload: {"value": out["value"], "valu_floor_frac": roof["frac"],
+                                "kernel_ms": m["avg_launch_ms"], "steps": args.steps}}
+        for name, v in side.items():
+            summ[name] = {"value": v["value"], "valu_floor_frac": v["valu_floor_frac"],
+                          "kernel_ms": v["dominant_avg_ms"], "steps": v["steps"]}
+        if cluster and cluster.get("value") is not None:
+            summ["cluster"] = {"value": cluster.get("value"), "clients": cluster.get("clients")}
+        out["summary"] = {"build": build, "workloads": summ}
+        # the full records (every CPU leg's sample text, whole rocprof summaries, cluster details) on stderr
+        log("bench detail: " + json.dumps({"cpu_baseline": cpu, "per_format_cpu": side_cpu, "cluster": cluster,
+                                           "rocprof": counters}))
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

@@ -10,12 +10,12 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 ALL_DEVICES = -1
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
 FLAG_NEVER_MATCHES, FLAG_REF_NONDETERMINISTIC = 1, 2
-MAX_PW, MAX_PW_RANGE = 64, 32
+MAX_PW, MAX_PW_RANGE, MAX_PW_R6 = 131071, 32, 176
 
 EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_device_list", "dprf_ctx_create",
            "dprf_ctx_create_devices", "dprf_ctx_destroy", "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel",

@@ -124,8 +124,10 @@ class Checkpoint:
 
 def first_round(kernel, ndev):
     """Candidates of the first range-mode round: ROUND_CHUNKS first chunks per device (the library's policy before
-    a rate is measured, dprf_plan_chunk), so no device idles in round 1 and its guided tail stays short."""
-    if not ROUND_CHUNKS or kernel is None:
+    a rate is measured, dprf_plan_chunk), so no device idles in round 1 and its guided tail stays short.  One device
+    has no guided tail: its rounds stay at FIRST_ROUND / ROUND_SECONDS, the checkpoint and Ctrl-C granularity
+    (ADVICE r3)."""
+    if not ROUND_CHUNKS or kernel is None or ndev <= 1:
         return FIRST_ROUND
     return max(FIRST_ROUND, ROUND_CHUNKS * ndev * _lib.plan_chunk(kernel, 0.0, _HUGE, _HUGE, 1))
 
@@ -135,7 +137,7 @@ def round_seconds(kernel, rate, ndev):
     library's largest chunk at the per-device rate if that is longer, so the guided tail of a call (chunks
     shrinking to the family's floor, include/dprf.h dprf_plan_chunk) stays a small part of the round."""
     per_dev_ms = rate / 1e3 / max(1, ndev)
-    if per_dev_ms <= 0 or not ROUND_CHUNKS or kernel is None:
+    if per_dev_ms <= 0 or not ROUND_CHUNKS or kernel is None or ndev <= 1:
         return ROUND_SECONDS
     big = _lib.plan_chunk(kernel, per_dev_ms, _HUGE, _HUGE, 1)
     return max(ROUND_SECONDS, ROUND_CHUNKS * big / per_dev_ms / 1e3)

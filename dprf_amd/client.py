@@ -81,7 +81,8 @@ class GpuVerifier:
 
     def __call__(self, stream, blob, offsets):
         """(found, password) for one payload, found = the lowest list index that verifies.  A payload with
-        candidates the format cannot take (NUL, empty or invalid-UTF-8 Office passwords, over 64 bytes) is
+        candidates the reference cannot verify (NUL, empty or invalid-UTF-8 Office passwords, PDF R6 over 176
+        bytes where the reference aborts, over an argv string's 131,071 bytes; include/dprf.h) is
         verified without them -- the reference fails such a candidate in its own verifier process and goes
         on with the rest (brute_force.py:106-161) -- instead of failing the payload on every client."""
         import numpy as np

@@ -152,11 +152,75 @@ DEVI void sha256_msg2(uint32_t m[32], uint32_t total, uint32_t out[8]) {
 /* The file is compiled three times (Makefile): the Office kernels (DPRF_PART_OFFICE), the ODF kernels
  * (DPRF_PART_ODT) and the PDF R2-R5 kernels (DPRF_PART_PDF), each object with the LLVM machine-scheduler
  * strategy that measured fastest for it AND leaves its kernels without scratch (resource_gate.py). */
-#if !defined(DPRF_PART_OFFICE) && !defined(DPRF_PART_ODT) && !defined(DPRF_PART_PDF)
+#if !defined(DPRF_PART_OFFICE) && !defined(DPRF_PART_ODT) && !defined(DPRF_PART_PDF) && !defined(DPRF_PART_LONG)
 #define DPRF_PART_OFFICE
 #define DPRF_PART_ODT
 #define DPRF_PART_PDF
+#define DPRF_PART_LONG
 #endif
+
+#ifdef DPRF_PART_LONG
+/* ================================================================== long candidates (round 4) */
+/* Candidates longer than the 64-byte list slot: the reference hashes any strlen(password) -- ODF's start key
+ * (odt...c:78-79), Office's H0 over salt || UTF-16LE (msoffcrypto...c:94-101, iconv of any length :275-336), PDF R5
+ * after truncation at 127 (pdf...c:197-206) and R6's K0 over the whole password (:240-245, <= 176 bytes, :228).  This
+ * kernel computes that first message's hash for one record per lane, streaming the record from the blob in 64-byte
+ * blocks (a lane loops over its own block count; records are rare, so the divergence costs nothing that matters);
+ * the format's usual kernels then run from the hash in `keys` (Office / ODF KDF, R6), or it compares directly (R5).
+ * Records sit 16-byte aligned in the blob, zero past their length; message words are built with static indices only. */
+DEVI uint32_t long_msg_word(const uint32_t *rec, uint32_t len, uint32_t dw, const uint32_t sw[3], uint32_t ns) {
+    /* LE word dw of record || suffix bytes || 0x80: the suffix words sw[0..ns) (ns - 1 suffix words + the 0x80 word)
+     * land at byte offset len */
+    uint32_t v = 4u * dw < len ? rec[dw] & le_keep_mask(0, len - 4u * dw) : 0u;
+    const uint32_t q = len >> 2, r = (len & 3u) * 8u;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+        if (k >= ns) break;
+        if (dw == q + k) v |= sw[k] << r;
+        if (r && dw == q + k + 1u) v |= sw[k] >> (32u - r);
+    }
+    return v;
+}
+__global__ void __launch_bounds__(256)
+k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= e.count) return;
+    const uint64_t rec = e.start + g;
+    const uint32_t *d = e.slots + e.loff[rec];
+    const uint32_t len = e.llen[rec];
+    const bool sha1 = lp.alg == DPRF_LONG_SHA1_SALT16;
+    const uint32_t prew = sha1 ? 4u : 0u;                                /* message words before the record */
+    const bool salt = lp.alg == DPRF_LONG_SHA256_SALT8 || lp.alg == DPRF_LONG_R5;
+    const uint32_t sw[3] = {salt ? lp.suffix[0] : 0x80u, salt ? lp.suffix[1] : 0u, 0x80u};
+    const uint32_t ns = salt ? 3u : 1u;
+    const uint32_t total = 4u * prew + len + (salt ? 8u : 0u);           /* message bytes */
+    const uint32_t nb = (total + 9u + 63u) >> 6;                        /* blocks incl. 0x80 and the bit length */
+    uint32_t h[8];
+    if (sha1) { sha1_iv(h); h[5] = h[6] = h[7] = 0u; }
+    else sha256_iv(h);
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t t = 16u * b + (uint32_t)j;
+            w[j] = t < prew ? lp.prefix[j & 3] : bswap32(long_msg_word(d, len, t - prew, sw, ns));
+        }
+        if (b + 1u == nb) { w[14] = 0u; w[15] = total * 8u; }
+        if (sha1) sha1_compress(h, w);
+        else sha256_compress(h, w);
+    }
+    if (lp.alg == DPRF_LONG_R5) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < 8; k++) ok = ok && h[k] == lp.target[k];
+        if (ok) report_hit(R, rec, cap, stop_on_first);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (k < 5 || !sha1) e.keys[(size_t)k * e.count + g] = h[k];
+}
+#endif /* DPRF_PART_LONG */
 
 #ifdef DPRF_PART_OFFICE
 /* ================================================================== Office (ECMA-376 Standard) */
@@ -173,15 +237,20 @@ k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_o
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (g0 >= e.count) return;
     const uint32_t g = g0;
-    cand c;
-    get_candidate<MODE, true>(e, cs, g, c);
-
-    /* H0 = SHA1(salt[0:16] || UTF16LE(pw)) (msoffcrypto...c:94-101) */
-    uint32_t m[32];
-    m[0] = p.salt[0]; m[1] = p.salt[1]; m[2] = p.salt[2]; m[3] = p.salt[3];
-    be_append<4>(m, c);
     uint32_t h[5];
-    sha1_msg2(m, 16u + c.len, h);
+    if constexpr (MODE == 2) {
+        /* long list: H0 from k_long_prehash (same place this kernel leaves X1: the lane's own column) */
+#pragma unroll
+        for (int k = 0; k < 5; k++) h[k] = keys[(size_t)k * e.count + g];
+    } else {
+        cand c;
+        get_candidate<MODE, true>(e, cs, g, c);
+        /* H0 = SHA1(salt[0:16] || UTF16LE(pw)) (msoffcrypto...c:94-101) */
+        uint32_t m[32];
+        m[0] = p.salt[0]; m[1] = p.salt[1]; m[2] = p.salt[2]; m[3] = p.salt[3];
+        be_append<4>(m, c);
+        sha1_msg2(m, 16u + c.len, h);
+    }
 
     /* 50,000 x H = SHA1(LE32(i) || H) (:105-113): W0 = bswap(i) is wave-uniform */
     for (uint32_t i = 0; i < 50000u; i++) {
@@ -268,12 +337,15 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (g0 >= e.count) return;
     const uint32_t g = g0;
-    cand c;
-    get_candidate<MODE, false>(e, cs, g, c);
-
     /* start key = SHA256(password) (odt...c:78-79) */
     uint32_t sk[8];
-    {
+    if constexpr (MODE == 2) {
+        /* long list: from k_long_prehash, in the lane's own key column */
+#pragma unroll
+        for (int k = 0; k < 8; k++) sk[k] = keys[(size_t)k * e.count + g];
+    } else {
+        cand c;
+        get_candidate<MODE, false>(e, cs, g, c);
         uint32_t m[32];
         be_append<0>(m, c);
         sha256_msg2(m, c.len, sk);
@@ -884,7 +956,8 @@ hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const 
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
     if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
-    else hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else if (e.mode == 1) hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_office_kdf<2>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
@@ -896,12 +969,21 @@ hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_a
                       dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
     if (e.mode == 0) hipLaunchKernelGGL(k_odt_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
-    else hipLaunchKernelGGL(k_odt_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else if (e.mode == 1) hipLaunchKernelGGL(k_odt_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_odt_kdf<2>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_odt_check, GRID(e.count, ODT_CHECK_THREADS), dim3(ODT_CHECK_THREADS), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
 }
 #endif /* DPRF_PART_ODT */
+
+#ifdef DPRF_PART_LONG
+hipError_t launch_long_prehash(const dprf_enum &e, const dprf_long_params &lp, dprf_results *R, uint32_t cap,
+                               uint32_t stop, hipStream_t s) {
+    hipLaunchKernelGGL(k_long_prehash, GRID(e.count, 256), dim3(256), 0, s, e, lp, R, cap, stop);
+    return hipGetLastError();
+}
+#endif
 
 #ifdef DPRF_PART_PDF
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,

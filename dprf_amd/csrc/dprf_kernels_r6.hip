@@ -378,10 +378,23 @@ DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const ui
 
 /* Load candidate `idx` (keyspace index or slot), compute K = SHA256(pw || salt), write pw to the
  * head of the lane's pattern column.  Returns the password length. */
+/* MODE 2 (long list, round 4): the record (<= 176 bytes, pdf...c:228) is copied word by word into the period column
+ * and K0 comes from k_long_prehash (keys, [8][ncand], launch-local candidate `off`). */
 template <int MODE>
 DEVI uint32_t r6_begin(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *cs, const uint8_t *sdig,
                        uint64_t idx, uint32_t off, const uint32_t *slots, const uint8_t *lens, const r6_lds &S,
-                       uint32_t K[16]) {
+                       uint32_t K[16], const uint64_t *loff = nullptr, const uint32_t *llen = nullptr,
+                       const uint32_t *keys = nullptr, uint32_t ncand = 0) {
+    if constexpr (MODE == 2) {
+        const uint32_t len = llen[idx];
+        const uint32_t *rec = slots + loff[idx];
+        for (uint32_t k = 0; k < ((len + 3u) >> 2); k++) *L32(S.pat + ((k << 8) | S.lanebase)) = rec[k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) K[k] = keys[(size_t)k * ncand + off];
+#pragma unroll
+        for (int k = 8; k < 16; k++) K[k] = 0u;
+        return len;
+    }
     uint32_t w[DPRF_SLOT_WORDS];
 #pragma unroll
     for (int j = 0; j < DPRF_SLOT_WORDS; j++) w[j] = 0;
@@ -651,6 +664,9 @@ struct r6_shared {
     uint32_t nslots, te_slots, ncand, pat_words;
     const uint32_t *slots;                    /* e.slots, e.lens (list mode), likewise */
     const uint8_t *lens;
+    const uint64_t *loff;                     /* e.loff, e.llen, e.keys (long list mode) */
+    const uint32_t *llen;
+    const uint32_t *keys;
     unsigned long long start;                 /* e.start / e.count (ncand) read from here when a slot takes or reports a
                                                  candidate: kept in registers across the persistent loop, the
                                                  64-bit start was spilled to scratch (SGPR pressure) */
@@ -727,7 +743,8 @@ DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
     sh->cand[slot] = c;
     if (c == R6_IDLE) return false;
     uint32_t K[16];
-    const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, lds_load64(&sh->start) + c, c, sh->slots, sh->lens, S, K);
+    const uint32_t len = r6_begin<MODE>(e, p, cs, sh->sdig, lds_load64(&sh->start) + c, c, sh->slots, sh->lens, S, K,
+                                        sh->loff, sh->llen, sh->keys, lds_load(&sh->ncand));
     r6_store_k(S, len, 32u, K, MODE == 0 ? 4u * lds_load(&sh->pat_words) : ~0u);   /* list mode: full wrap */
     sh->state[slot] = len | (32u << 8);
     return true;
@@ -845,6 +862,9 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         sh->pat_words = pat_words;
         sh->slots = e.slots;
         sh->lens = e.lens;
+        sh->loff = e.loff;
+        sh->llen = e.llen;
+        sh->keys = e.keys;
     }
     __syncthreads();
 
@@ -984,13 +1004,14 @@ static uint32_t r6_pat_words(uint32_t mode, uint32_t lmax) {
 
 #define R6_MAX_DEVICES 64
 static std::mutex r6_attr_mu;
-static bool r6_attr_set[2][R6_MAX_DEVICES];
+static bool r6_attr_set[3][R6_MAX_DEVICES];
 
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s) {
     /* longest password of the launch (list mode: the host's maximum over the chunk): the period length
      * and with it the slots per CU follow the actual candidates, not the 64-byte slot width */
-    const uint32_t lmax = e.pwlen < 4u * DPRF_SLOT_WORDS ? e.pwlen : 4u * DPRF_SLOT_WORDS;
+    const uint32_t lcap = e.mode == 2 ? (uint32_t)DPRF_R6_MAX_LONG : 4u * DPRF_SLOT_WORDS;
+    const uint32_t lmax = e.pwlen < lcap ? e.pwlen : lcap;
     const uint32_t pat_words = r6_pat_words(e.mode, lmax);
     uint32_t nslots = 0, te_slots = 0;
     size_t shm = 0;
@@ -1014,12 +1035,13 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     /* one workgroup per CU; a launch smaller than the slots it would open uses fewer workgroups */
     uint32_t grid = (e.count + nslots - 1) / nslots;
     if (grid > (uint32_t)ncu) grid = (uint32_t)ncu;
-    const void *fn = e.mode == 0 ? (const void *)k_pdf_r6<0> : (const void *)k_pdf_r6<1>;
+    const void *fn = e.mode == 0 ? (const void *)k_pdf_r6<0> : e.mode == 1 ? (const void *)k_pdf_r6<1>
+                                                                            : (const void *)k_pdf_r6<2>;
     {
         /* function attributes are per device: set once per (device, mode), under a lock -- the device
          * workers of a multi-device context launch concurrently */
         std::lock_guard<std::mutex> g(r6_attr_mu);
-        bool &done = r6_attr_set[e.mode == 0 ? 0 : 1][dev];
+        bool &done = r6_attr_set[e.mode < 3 ? e.mode : 2][dev];
         if (!done) {
             me = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - R6_TE_BYTES);
             if (me != hipSuccess) return me;
@@ -1029,8 +1051,11 @@ hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dpr
     if (e.mode == 0)
         hipLaunchKernelGGL(k_pdf_r6<0>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots,
                            te_slots, idle_ticks);
-    else
+    else if (e.mode == 1)
         hipLaunchKernelGGL(k_pdf_r6<1>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots,
+                           te_slots, idle_ticks);
+    else
+        hipLaunchKernelGGL(k_pdf_r6<2>, dim3(grid), dim3(lanes), shm, s, e, p, T, R, cap, stop, pat_words, nslots,
                            te_slots, idle_ticks);
     return hipGetLastError();
 }

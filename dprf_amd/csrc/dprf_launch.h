@@ -16,6 +16,9 @@ hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_resu
                          uint32_t stop, hipStream_t s);
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                           uint32_t stop, hipStream_t s);
+/* long list (e.mode 2): the records' first-message hash into e.keys, or (DPRF_LONG_R5) the whole R5 check */
+hipError_t launch_long_prehash(const dprf_enum &e, const dprf_long_params &lp, dprf_results *R, uint32_t cap,
+                               uint32_t stop, hipStream_t s);
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s);
 #endif

@@ -8,22 +8,41 @@
 
 #define DPRF_SLOT_WORDS 16          /* list-mode candidate slot: 64 bytes, LE-packed */
 #define DPRF_MAX_RANGE_LEN 32
+#define DPRF_R6_MAX_LONG 176        /* PDF R6 candidates: data[(128 + 64 + 48) * 64] holds 64 x (pw || K[0:64]) only up
+                                       to 176 bytes (pdf...c:228); longer ones abort the reference (stack smashing) */
 
 /* Candidate source for one launch.  Range mode: candidate g of the launch is global keyspace index
  * start + g, spelled over charset in itertools.product order.  List mode: candidate g is slot
- * start + g of the device candidate buffer. */
+ * start + g of the device candidate buffer.  Long-list mode (round 4): candidate g is record start + g of a packed
+ * blob of candidates longer than a slot -- k_long_prehash hashes the record's first message (Office H0, the ODF
+ * start key, PDF R5's whole hash, R6's K0) into `keys`, and the format's kernels continue from there. */
 struct dprf_enum {
     uint64_t start;
     uint32_t count;
-    uint32_t mode;                  /* 0 range, 1 list */
-    uint32_t pwlen;                 /* range: fixed length (bytes); list: longest candidate of the launch */
+    uint32_t mode;                  /* 0 range, 1 list, 2 long list */
+    uint32_t pwlen;                 /* range: fixed length (bytes); list / long list: longest candidate of the launch */
     uint32_t cslen;
     uint32_t div_m;                 /* u32 division by cslen: q = (mulhi(n,m) + ((n-mulhi)>>1)) >> s */
     uint32_t div_s;
     uint8_t sdig[DPRF_MAX_RANGE_LEN];   /* base-cslen digits of start, most significant first */
     uint8_t charset[256];
-    const uint32_t *slots;          /* list: [n][DPRF_SLOT_WORDS] LE words */
+    const uint32_t *slots;          /* list: [n][DPRF_SLOT_WORDS] LE words; long list: the record blob (LE words) */
     const uint8_t *lens;            /* list: [n] byte lengths */
+    const uint64_t *loff;           /* long list: [n] word offset of each record in the blob (16-byte aligned)    */
+    const uint32_t *llen;           /* long list: [n] byte length of each record                                  */
+    uint32_t *keys;                 /* long list: [8][count] prehash output (chunk-local), read by the next kernel */
+};
+
+/* Long-list prehash (k_long_prehash): the first message of the format's verify() over a record of any length. */
+#define DPRF_LONG_SHA1_SALT16 1     /* Office H0 = SHA1(salt[0:16] || UTF16LE(pw)) (msoffcrypto...c:94-101) -> keys[5] */
+#define DPRF_LONG_SHA256 2          /* ODF start key = SHA256(pw) (odt...c:78-79)                       -> keys[8] */
+#define DPRF_LONG_SHA256_SALT8 3    /* R6 K0 = SHA256(pw || salt8) (pdf...c:240-245)                    -> keys[8] */
+#define DPRF_LONG_R5 4              /* R5: SHA256(pw[:127] || salt8) == U[0:32] (pdf...c:194-221)       -> hits    */
+struct dprf_long_params {
+    uint32_t alg;                   /* DPRF_LONG_*                                                          */
+    uint32_t prefix[4];             /* SHA1_SALT16: the salt as BE words (message words 0..3)               */
+    uint32_t suffix[2];             /* SALT8 / R5: the 8 salt bytes as LE words, appended after the record  */
+    uint32_t target[8];             /* R5: U[0:32] as BE words                                              */
 };
 
 /* Device results of one API call (accumulated over its launches). */

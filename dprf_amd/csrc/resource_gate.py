@@ -6,7 +6,11 @@ this script on them.  It fails the build when a kernel spills to scratch beyond 
 compiler-flag or source change that starts spilling cannot ship silently (round 2 shipped k_odt_kdf with
 20 B/lane of scratch under the max-ilp scheduler: 1.46x its algorithmic HBM writes).
 
-Usage: resource_gate.py <file.res>...   (prints one line per kernel; exit 1 on a violation)
+Usage: resource_gate.py [--expect k1,k2,...] <file.res>...   (one line per kernel; exit 1 on a violation)
+
+The gate fails closed (round 4): a remark block without a ScratchSize line, a report with no kernel in
+it, or an expected kernel (--expect, the Makefile passes each object's kernel families) missing from the report
+all fail the build -- a changed remark format or a dropped -Rpass-analysis flag must not read as "0 B of scratch".
 """
 import re
 import subprocess
@@ -24,6 +28,7 @@ SCRATCH_LIMIT = {
     "k_pdf_r5": 0,
     "k_pdf_r24": 0,
     "k_pdf_r6": 0,
+    "k_long_prehash": 0,      # round 4: candidates longer than a list slot
 }
 
 
@@ -49,15 +54,28 @@ def demangle(names):
     return {n: (out[i] if i < len(out) and out[i] else n) for i, n in enumerate(names)}
 
 
-def main(paths):
-    bad = []
+def main(argv):
+    bad, expect, paths = [], set(), []
+    it = iter(argv)
+    for a in it:
+        if a == "--expect":
+            expect |= {x for x in next(it, "").split(",") if x}
+        else:
+            paths.append(a)
+    seen = set()
     for path in paths:
         rows = parse(open(path).read())
+        if not rows:
+            bad.append("%s: no kernel in the resource report" % path)
         dem = demangle(list(rows))
         for mangled, r in rows.items():
             name = dem[mangled].split("(")[0]
             full = re.sub(r"^void ", "", name)
-            scratch = int(r.get("ScratchSize [bytes/lane]", "0"))
+            seen.add(full.split("<")[0])
+            if "ScratchSize [bytes/lane]" not in r:
+                bad.append("%s (no ScratchSize remark)" % name)
+                continue
+            scratch = int(r["ScratchSize [bytes/lane]"])
             limit = SCRATCH_LIMIT.get(full.replace(" ", ""), SCRATCH_LIMIT.get(full.split("<")[0]))
             ok = limit is not None and scratch <= limit
             print("%-6s %-44s VGPRs %-4s scratch %-3d (limit %s) occupancy %s" % (
@@ -65,8 +83,10 @@ def main(paths):
                 r.get("Occupancy [waves/SIMD]")))
             if not ok:
                 bad.append(name)
+    for k in sorted(expect - seen):
+        bad.append("%s (expected, not in the report)" % k)
     if bad:
-        sys.stderr.write("resource_gate: scratch above the stated bound (or unknown kernel): %s\n" % ", ".join(bad))
+        sys.stderr.write("resource_gate: scratch above the stated bound, unknown or missing kernel, or no report: %s\n" % ", ".join(bad))
         return 1
     return 0
 

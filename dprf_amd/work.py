@@ -81,6 +81,7 @@ FLOOR = {
     "sha1c_office_loop": sha1_floor(range(6, 16), (0,)),       # W0 = bswap(i) uniform, W1..W5 = H
     "sha1c_hmac20": sha1_floor(range(5, 16)),                  # PBKDF2 iteration: 20-byte message
     "sha256c": sha256_floor(), "sha512c": sha512_floor(), "md5c": md5_floor(), "md5c_16": md5_floor(12),
+    "md5c_5": md5_floor(14),                                   # 5-byte message (R3 40-bit): words 2..15 constant
     "aes128_enc_block": 9 * AES_ROUND + AES_LAST + 4 * COST["xor"] + 4 * COST["xor"],   # + CBC xor
     "aes128_dec_block": 9 * AES_ROUND + AES_LAST + 4 * COST["xor"],
     "aes256_dec_block": 13 * AES_ROUND + AES_LAST + 8 * COST["xor"],                    # + CBC xor
@@ -95,7 +96,7 @@ FLOOR = {
 }
 SPEC = {
     "sha1c": 1001, "sha1c_office_loop": 1001, "sha1c_hmac20": 1001, "sha256c": 2296, "sha512c": 5840,
-    "md5c": 532, "md5c_16": 532, "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
+    "md5c": 532, "md5c_16": 532, "md5c_5": 532, "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
     "aes128_keyexp": 0, "aes128_dec_sched": 0, "aes256_keyexp_dec_sched": 0, "rc4_ksa": 2304, "rc4_prga_byte": 16,
 }
 
@@ -113,6 +114,8 @@ COUNTS = {
     # PDF R3/R4: initial MD5 2 blocks + 50 (16-byte message); 20 x (KSA + 16 PRGA bytes).
     # MD5(PAD || ID) is document-constant (the reference recomputes it per candidate, :167); not counted.
     "pdf_r34": {"md5c": 2, "md5c_16": 50, "rc4_ksa": 20, "rc4_prga_byte": 320},
+    # R3 with a 40-bit key (EVP_rc4_40, pdf...c:445-453): the 50 MD5s hash 5 bytes, the RC4 passes use 5-byte keys
+    "pdf_r3_40": {"md5c": 2, "md5c_5": 50, "rc4_ksa": 20, "rc4_prga_byte": 320},
     "pdf_r2": {"md5c": 2, "rc4_ksa": 1, "rc4_prga_byte": 32},
     "pdf_r5": {"sha256c": 1},
     # PDF R6, L = 6: mean over 1,000 random lowercase candidates (69.9 rounds)
@@ -128,8 +131,8 @@ MAIN = {
 # which resource bounds each format when no current rocprof profile says otherwise.  The RC4 formats saturate
 # neither pipe (R3/R4 VALUBusy 0.73, LdsUtil 0.52: each wave's KSA is a chain of one dependent LDS round trip per
 # two steps); VALU is the busier of the two, so that is what their fraction is quoted against.
-BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "valu", "pdf_r2": "valu", "pdf_r5": "valu",
-         "pdf_r6": "valu"}
+BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "valu", "pdf_r3_40": "valu", "pdf_r2": "valu",
+         "pdf_r5": "valu", "pdf_r6": "valu"}
 
 
 # LDS-array cycles per candidate of the RC4 formats, from MI355X_MICROARCH.md's LDS table: every byte / u16 / dword
@@ -145,6 +148,7 @@ BOUND = {"office": "valu", "odt": "valu", "odt_e": "valu", "pdf_r34": "valu", "p
 #   R2: the same KSA + 4 PRGA bytes x (3 reads + 2 stores) x 2 + the hand-off 16.
 LDS_CYCLES = {
     "pdf_r34": (20 * ((64 + 256 + 256 + 128 + 127) * 2 + 10) + 16) / 64.0,
+    "pdf_r3_40": (20 * ((64 + 256 + 256 + 128 + 127) * 2 + 10) + 16) / 64.0,     # the same KSA schedule, 5-byte key
     "pdf_r2": ((64 + 256 + 256 + 128 + 127) * 2 + 4 * 5 * 2 + 16) / 64.0,
 }
 PEAK_LDS_CYCLES_PER_S = 256 * 2.4e9          # one LDS per CU

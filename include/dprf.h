@@ -18,6 +18,10 @@
  * brute_force.py:70-73 / :92-95, become one worker thread per GPU on one shared chunk cursor).  Calls on
  * DIFFERENT contexts may run concurrently from different threads; calls on the SAME context are
  * serialised by the library (a second caller waits for the first call to return).
+ * Every entry point leaves the calling thread's current HIP device as it found it (ABI 5): the library sets the
+ * device of each GPU it serves from the calling thread and restores the caller's on return, so a torch user's
+ * default device (torch.cuda.current_device()) is not moved by a call (client.py:94-108 treats the verifier as a
+ * pure call).
  * Ownership: the caller owns every buffer it passes; they are read/written only during the call.
  */
 #ifndef DPRF_H
@@ -28,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 4
+#define DPRF_ABI_VERSION 5
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -42,7 +46,8 @@ extern "C" {
                                     undefined or an abort() there           */
 #define DPRF_E_HIP (-3)          /* HIP runtime error (message has the hipError string)           */
 #define DPRF_E_NODEVICE (-4)     /* no usable gfx950 device / bad device ordinal                  */
-#define DPRF_E_PWLEN (-5)        /* candidate longer than the kernel supports (see DPRF_MAX_PW)    */
+#define DPRF_E_PWLEN (-5)        /* candidate too long: over DPRF_MAX_PW bytes (list mode; no argv string can carry
+                                    it to the reference), or a range length over DPRF_MAX_PW_RANGE  */
 #define DPRF_E_CHARSET (-6)      /* charset invalid for this format (e.g. non-ASCII for Office)    */
 
 #define DPRF_ALL_DEVICES (-1)    /* dprf_ctx_create device argument: every gfx950 device visible    */
@@ -56,10 +61,18 @@ extern "C" {
                                             (BN_hex2bn/BN_bn2bin) decodes it short and reads
                                             uninitialised bytes; this library decodes it in full.   */
 
-/* Longest candidate the kernels accept, in bytes of the password as given (UTF-8).  Office counts
- * UTF-16 code units instead (<= 32).  PDF R2-R4 truncate at 32 bytes like the reference
- * (pdf...c:137), so longer candidates are accepted there. */
-#define DPRF_MAX_PW 64
+/* List mode takes every candidate the reference's verifiers hash (ABI 5; ABI 4 capped them at a 64-byte slot):
+ * ODF and Office any length (odt...c:79 hashes strlen(password); msoffcrypto...c:75,287-296 converts any length to
+ * UTF-16LE), PDF R2-R4 truncated at 32 bytes (pdf...c:137), R5 at 127 (:197-206), R6 whole up to DPRF_MAX_PW_R6.
+ * Candidates up to 64 bytes after conversion run in 64-byte slots; longer ones go to a long sub-list (k_long_prehash
+ * hashes their first message, the format's kernels continue from it) -- same verdicts, same list indices.
+ * DPRF_MAX_PW: the reference receives a candidate as one argv string, which Linux caps at MAX_ARG_STRLEN (131,072
+ * bytes with the NUL): a longer one never reaches its verifier (DPRF_E_PWLEN).
+ * DPRF_MAX_PW_R6: 64 x (pw || K[0:64]) fills the reference's data[(128 + 64 + 48) * 64] (pdf...c:228) at 176 bytes; a
+ * longer R6 candidate overflows it and the reference aborts ("stack smashing detected", recorded in
+ * tests/golden/long_verdicts.json) -- an error, not a verdict, so DPRF_E_DOMAIN. */
+#define DPRF_MAX_PW 131071
+#define DPRF_MAX_PW_R6 176
 #define DPRF_MAX_PW_RANGE 32   /* longest fixed length for dprf_search_range */
 
 typedef struct dprf_ctx dprf_ctx;
@@ -148,8 +161,9 @@ int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwle
  * Candidate k is blob[offsets[k] .. offsets[k+1]) (n+1 offsets).  Hits are list indices. */
 int dprf_verify_list(dprf_ctx *ctx, const uint8_t *blob, const uint64_t *offsets, int64_t n,
                      int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits, dprf_stats *stats);
-/* dprf_verify_list rejects the whole call if one candidate is invalid for the format (NUL, empty or
- * invalid-UTF-8 Office password, longer than DPRF_MAX_PW after truncation).  This host-only check (no
+/* dprf_verify_list rejects the whole call if one candidate is one the reference cannot verify (NUL; empty or
+ * invalid-UTF-8 Office password; PDF R6 over DPRF_MAX_PW_R6 bytes: DPRF_E_DOMAIN / DPRF_E_INVALID; over DPRF_MAX_PW
+ * bytes: DPRF_E_PWLEN).  This host-only check (no
  * device work) writes 0 or that DPRF_E_* code per candidate to status[n] (may be NULL) and returns the
  * number of invalid candidates, so a caller can drop them and verify the rest -- the reference fails
  * such a candidate alone, in its own verifier process (brute_force.py:163-197).  (ABI 3) */

@@ -570,15 +570,17 @@ static int utf8_to_utf16le(const uint8_t *s, int n, uint8_t *out, int cap) {
 /* Office: verify() msoffcrypto_password_verifier.c:56-191.  inter (may be NULL) receives
  * finalH[20] | X1[20] | key[16] | sha1(verifier)[20] | dec_evh[0:20] */
 static int verify_office(const orc_ctx *c, const uint8_t *pw, int len, uint8_t *inter) {
-    uint8_t u16[512];
     if (len <= 0) return -1;                 /* iconv of "" -> -1, then uninitialised length (:287-292) */
-    int ulen = utf8_to_utf16le(pw, len, u16, (int)sizeof u16);
-    if (ulen < 0) return -1;                 /* iconv failure: reference continues on freed memory */
+    /* any length (iconv's buffer grows, :306-323): 2 bytes of UTF-16LE per UTF-8 byte at most */
+    uint8_t *u16 = (uint8_t *)malloc((size_t)len * 2);
+    int ulen = utf8_to_utf16le(pw, len, u16, len * 2);
+    if (ulen < 0) { free(u16); return -1; }  /* iconv failure: reference continues on freed memory */
     /* H0 = SHA1(salt[0:16] || pwU16) over salt_len + ulen bytes, zero tail (:94-101) */
     size_t mlen = (size_t)c->salt_len + (size_t)ulen;
     uint8_t *msg = (uint8_t *)calloc(mlen, 1);
     memcpy(msg, c->salt, 16);
     memcpy(msg + 16, u16, (size_t)ulen);
+    free(u16);
     uint8_t h[20], tmp[24];
     orc_sha1(msg, mlen, h);
     free(msg);
@@ -694,6 +696,9 @@ static int verify_pdf(const orc_ctx *c, const uint8_t *pw, int len, uint8_t *int
         return memcmp(hh, c->u, 32) == 0;
     }
     if (R == 6) {                                                        /* :115-132 */
+        /* data[(128 + 64 + 48) * 64] (:228) holds 64 x (pw || K[0:64]) up to pwlen 176; longer passwords overflow it
+         * and the reference aborts (stack protector, measured: tests/golden/long_verdicts.json) */
+        if (len > 176) return -1;
         uint8_t hh[32];
         pdf_r6_hash(pw, len, c->u + 32, hh);
         if (inter) memcpy(inter, hh, 32);

@@ -42,6 +42,12 @@ def intermediates():
 
 
 @pytest.fixture(scope="session")
+def long_verdicts():
+    """Reference verdicts for long candidates (tests/golden/make_long.py): name -> {stream, password, verdicts}"""
+    return load_golden("long_verdicts.json")
+
+
+@pytest.fixture(scope="session")
 def oracle():
     import pyoracle
     pyoracle.lib()

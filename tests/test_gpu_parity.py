@@ -35,22 +35,9 @@ def test_kernel_families(dprf, streams):
             assert fam == want[name.split("_")[0]], (name, fam)
 
 
-def device_limit_ok(name, pw, streams):
-    """Candidates the kernels take (DPRF_MAX_PW): Office <= 32 UTF-16 code units, PDF R2-R4 any length
-    (truncated at 32 like the reference), R5 <= 64 bytes after its 127-byte truncation, others <= 64 bytes."""
-    b = pw.encode()
-    s = streams[name]["stream"]
-    if "$office$" in s:
-        return len(pw.encode("utf-16-le")) <= 64
-    if "$pdf$*" in s and s.split("*")[2] in ("2", "3", "4"):
-        return True
-    return len(b) <= 64
-
-
 def test_verdict_tables_match_reference(dprf, streams, verdicts):
     for name, table in verdicts.items():
         c = ctx_for(dprf, streams, name)
-        table = [(p, v) for p, v in table if device_limit_ok(name, p, streams)]
         cands = [p for p, _ in table]
         hits, n, st = c.verify_list(cands)
         want = [i for i, (_, v) in enumerate(table) if v]
@@ -58,14 +45,74 @@ def test_verdict_tables_match_reference(dprf, streams, verdicts):
         assert st["candidates"] == len(cands)
 
 
-def test_over_limit_candidates_raise(dprf, streams, verdicts):
-    for name, table in verdicts.items():
-        over = [p for p, _ in table if not device_limit_ok(name, p, streams)]
-        if not over:
-            continue
-        with pytest.raises(dprf.DprfError) as ei:
-            ctx_for(dprf, streams, name).verify_list(over)
-        assert ei.value.code == dprf.E_PWLEN
+def _long_ctx(dprf, d, devices=None):
+    from dprf_amd import brute_force as bf
+    return dprf.Context(bf.parse_verification_data(d["stream"]), devices=devices)
+
+
+def test_long_candidates_match_reference(dprf, long_verdicts):
+    """Round 4: candidates of 64/65/119/120/127/128/176 bytes and multi-byte UTF-8 (2-, 3-, 4-byte
+    sequences) on documents whose passwords are long themselves (tests/golden/make_long.py): the GPU's hits equal the
+    reference executables' exit codes, short and long candidates mixed in one list.  R6 candidates over 176 bytes,
+    where the reference aborts (-6) or crashes (-11), are DPRF_E_DOMAIN -- in the status call and when verified."""
+    for name, d in long_verdicts.items():
+        ok = [(p, v) for p, v in d["verdicts"] if v in (0, 1)]
+        bad = [p for p, v in d["verdicts"] if v not in (0, 1)]
+        c = _long_ctx(dprf, d)
+        hits, n, st = c.verify_list([p for p, _ in ok])
+        want = [i for i, (_, v) in enumerate(ok) if v]
+        assert hits == want and n == len(want), (name, [ok[i][0] for i in hits], [ok[i][0] for i in want])
+        assert st["candidates"] == len(ok)
+        assert any(len(p.encode()) > 64 for p, _ in ok), name
+        if bad:
+            from dprf_amd import payload as pl
+            blob, offs = pl._pack(bad)
+            assert [int(v) for v in c.list_status(blob, offs)] == [dprf.E_DOMAIN] * len(bad), name
+            with pytest.raises(dprf.DprfError) as ei:
+                c.verify_list(bad[:1])
+            assert ei.value.code == dprf.E_DOMAIN
+        c.close()
+
+
+def test_long_and_short_lowest_hit_across_sub_lists(dprf, long_verdicts):
+    """stop_on_first over a list mixing slot-sized and long candidates: the answer is the lowest list index that
+    verifies, whichever sub-list (slots or long records) holds it; list indices survive the split; two device lanes
+    give the same answer."""
+    d = long_verdicts["pdf_r5_long127"]
+    pw = d["password"]
+    rng = random.Random(3)
+    words = ["".join(rng.choice(ALNUM) for _ in range(rng.choice((5, 40, 70, 100, 130)))) for _ in range(3000)]
+    plant = {1717: pw + "-beyond-127-is-ignored", 2400: pw}
+    for k, v in plant.items():
+        words[k] = v
+    for devs in ([0], [0, 0]):
+        c = _long_ctx(dprf, d, devs)
+        hits, n, st = c.verify_list(words)
+        assert hits == sorted(plant) and n == 2 and st["candidates"] == len(words)
+        h1, _, _ = c.verify_list(words, stop_on_first=True, cap=1)
+        assert h1 == [1717]
+        c.close()
+
+
+def test_long_list_over_several_launches(dprf, oracle, long_verdicts):
+    """A long sub-list of 2^20 + 3 records (more than one long-list launch, LONG_HI = 2^20): 130-byte R5 candidates,
+    which the reference truncates to 127 (pdf...c:197-200), with the 127-byte password as the prefix of four of them
+    planted across the launch seam, and a near miss (last kept byte changed)."""
+    import numpy as np
+    d = long_verdicts["pdf_r5_long127"]
+    pw = np.frombuffer(d["password"].encode(), dtype=np.uint8)
+    n = (1 << 20) + 3
+    blob = np.random.default_rng(5).integers(65, 91, size=(n, 130), dtype=np.uint8)
+    plant = [0, (1 << 20) - 1, 1 << 20, n - 1]
+    for k in plant + [7]:
+        blob[k, :127] = pw
+    blob[7, 126] ^= 1
+    offs = np.arange(n + 1, dtype=np.uint64) * 130
+    c = _long_ctx(dprf, d)
+    hits, nh, st = c.verify_blob(blob.tobytes(), offs)
+    assert hits == plant and nh == len(plant) and st["candidates"] == n and st["launches"] >= 2
+    assert oracle.Ctx(d["stream"]).verify(bytes(blob[7])) == 0 and oracle.Ctx(d["stream"]).verify(bytes(blob[0])) == 1
+    c.close()
 
 
 def test_hitsets_match_reference(dprf, streams, hitsets):
@@ -187,8 +234,12 @@ def test_errors_are_errors_not_hits(dprf, streams):
         c.search_range("aé", 2, 0, 4)
     assert ei.value.code == dprf.E_CHARSET
     c2 = ctx_for(dprf, streams, "pdf_synth_r6_ox")
+    c2.verify_list(["x" * 65, "y" * 176])                    # long candidates are verified (round 4)
     with pytest.raises(dprf.DprfError) as ei:
-        c2.verify_list(["x" * 65])
+        c2.verify_list(["x" * 177])                          # the reference overflows data[] and aborts
+    assert ei.value.code == dprf.E_DOMAIN
+    with pytest.raises(dprf.DprfError) as ei:
+        c.verify_list(["z" * (dprf.MAX_PW + 1)])            # no argv string carries it to the reference
     assert ei.value.code == dprf.E_PWLEN
     with pytest.raises(dprf.DprfError):
         c2.search_range(LOWER, 3, 26 ** 3 - 5, 10)
@@ -412,12 +463,62 @@ def test_list_status_marks_only_the_invalid_candidates(dprf, streams):
     from dprf_amd import client as cl
     from dprf_amd import payload as pl
     s = streams["office_testdoc"]["stream"]
-    pws = ["x", "", "bad\x00nul", "password", "y" * 40]
+    pws = ["x", "", "bad\x00nul", "password", "y" * 40, "z" * (dprf.MAX_PW + 1)]
     blob, offs = pl._pack(pws)
     with dprf.Context(__import__("dprf_amd.brute_force", fromlist=["x"]).parse_verification_data(s)) as c:
         st = c.list_status(blob, offs)
-        assert [int(v) for v in st] == [0, dprf.E_DOMAIN, dprf.E_INVALID, 0, dprf.E_PWLEN]
+        assert [int(v) for v in st] == [0, dprf.E_DOMAIN, dprf.E_INVALID, 0, 0, dprf.E_PWLEN]
     ver = cl.GpuVerifier([0])
     assert ver(s, blob, offs) == (1, "password")
     assert ver.skipped == 3
     ver.close()
+
+
+@pytest.mark.parametrize("name,length,skipped", [("odt_long_e_200", 200, 0), ("pdf_r6_long176", 176, 0),
+                                                 ("pdf_r6_long176", 200, 1)])
+def test_gpu_client_verifies_long_payloads(dprf, long_verdicts, name, length, skipped):
+    """the GPU client drops no candidate the reference verifies -- a payload of 200-byte ODF candidates
+    (and 176-byte R6 ones) is verified whole, the document's password among them is found.  Only what the reference
+    cannot verify is skipped: a 200-byte R6 candidate aborts the reference (data[] overflow)."""
+    from dprf_amd import client as cl
+    from dprf_amd import payload as pl
+    d = long_verdicts[name]
+    rng = random.Random(length)
+    pws = ["".join(rng.choice(ALNUM) for _ in range(length)) for _ in range(500)]
+    pws[321] = d["password"]
+    if skipped:
+        pws[17] = "q" * 200
+    blob, offs = pl._pack(pws)
+    ver = cl.GpuVerifier([0])
+    assert ver(d["stream"], blob, offs) == (1, d["password"])
+    assert ver.skipped == skipped and ver.verified == len(pws)
+    ver.close()
+
+
+def test_calls_leave_the_callers_device_alone(dprf, streams):
+    """every entry point restores the calling thread's HIP device (hipGetDevice through ctypes on
+    libamdhip64, which is what torch.cuda.current_device() reads).  With more than one GPU the caller sits on the LAST
+    device and the context spans every device, so a call that moved it would be seen."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    cur = ctypes.c_int(-1)
+
+    def get():
+        assert hip.hipGetDevice(ctypes.byref(cur)) == 0
+        return cur.value
+    ndev = dprf.device_count()
+    assert hip.hipSetDevice(ndev - 1) == 0
+    before = get()
+    from dprf_amd import brute_force as bf
+    fields = bf.parse_verification_data(streams["pdf_synth_r5_cat"]["stream"])
+    c = dprf.Context(fields, devices=list(range(ndev)) if ndev > 1 else [0, 0])
+    assert get() == before
+    c.search_range(LOWER, 3, 0, 26 ** 3)
+    assert get() == before
+    c.verify_list(["cat", "x" * 100])
+    assert get() == before
+    with pytest.raises(dprf.DprfError):
+        c.search_range(LOWER, 33, 0, 1)
+    assert get() == before
+    c.close()
+    assert get() == before

@@ -103,3 +103,19 @@ def test_never_matches_gate(oracle):
     c = oracle.Ctx(s)
     assert c.flags & oracle.FLAG_NEVER_MATCHES
     assert c.verify("anything") == 0
+
+
+def test_long_candidates_match_reference(oracle, long_verdicts):
+    """Round 4: candidates past the kernels' 64-byte slot (64..200 bytes, multi-byte UTF-8) on documents whose own
+    passwords are long (Office 70 / 104 bytes, ODF 100 / 200, R5 90 / 127 / 150, R6 100 / 140 / 176).  The reference's
+    exit code is matched exactly; where it aborts or crashes (R6 over 176 bytes overflows data[], pdf...c:228: -6 / -11)
+    the oracle reports the domain error (-1) the library turns into DPRF_E_DOMAIN."""
+    for name, d in long_verdicts.items():
+        ctx = oracle.Ctx(d["stream"])
+        assert ctx.verify(d["password"]) == 1, name
+        table = d["verdicts"]
+        got = ctx.verify_list([c for c, _ in table])
+        want = [v if v in (0, 1) else -1 for _, v in table]
+        assert got == want, (name, [(c, g, w) for (c, w), g in zip(table, got) if g != w])
+        if "pdf_r6" in name:
+            assert all((v < 0) == (len(c.encode()) > 176) for c, v in table), name

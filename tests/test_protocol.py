@@ -205,15 +205,26 @@ class _FakeCtx:
     def __init__(self, fields, devices=None):
         import pyoracle
         self.c = pyoracle.Ctx(fields)
+        self.fields = fields
         self.devices = devices
 
     def _status(self, p):
+        """dprf_list_status's rules (include/dprf.h, ABI 5): NUL; longer than an argv string; Office "" or invalid
+        UTF-8; PDF R6 over 176 bytes"""
         from dprf_amd import _lib
         if b"\x00" in p:
             return _lib.E_INVALID
-        if not p:
+        if len(p) > _lib.MAX_PW:
+            return _lib.E_PWLEN
+        if self.fields[0] == "office":
+            try:
+                p.decode("utf-8")
+            except UnicodeDecodeError:
+                return _lib.E_DOMAIN
+            return _lib.E_DOMAIN if not p else 0
+        if self.fields[0] == "pdf" and self.fields[2] == "6" and len(p) > _lib.MAX_PW_R6:
             return _lib.E_DOMAIN
-        return _lib.E_PWLEN if len(p.decode("utf-8", "replace").encode("utf-16-le")) > 64 else 0
+        return 0
 
     def list_status(self, blob, offsets):
         b = bytes(blob)
@@ -242,10 +253,10 @@ def test_gpu_verifier_drops_invalid_candidates_instead_of_failing(streams, monke
     monkeypatch.setattr(_lib, "Context", _FakeCtx)
     s = streams["office_testdoc"]["stream"]
     ver = cl.GpuVerifier(devices=[0])
-    pws = ["x", "", "bad\x00nul", "y" * 40, "password", "password"]
+    pws = ["x", "", "bad\x00nul", "y" * 40, "z" * (_lib.MAX_PW + 1), "password", "password"]
     blob, offs = pl._pack(pws)
     assert ver(s, blob, offs) == (1, "password")
-    assert ver.skipped == 3 and ver.verified == len(pws)
+    assert ver.skipped == 3 and ver.verified == len(pws)          # a 40-character candidate is verified (round 4)
     blob, offs = pl._pack(["a", "b"])
     assert ver(s, blob, offs) == (0, None)          # the valid-only path leaves clean payloads alone
     ver.close()

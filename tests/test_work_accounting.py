@@ -34,6 +34,10 @@ def test_pdf_rc4_counts(oracle, streams):
     # the reference recomputes the document-constant MD5(PAD || ID) per candidate (:167); COUNTS does not
     assert c["md5c"] == w["md5c"] + w["md5c_16"] + 1
     assert c["rc4_ksa"] == w["rc4_ksa"] and c["rc4_prga_bytes"] == w["rc4_prga_byte"]
+    c = _counts(oracle, streams, "pdf_synth_r3_l40_cab", "abcdefg")
+    w = work.COUNTS["pdf_r3_40"]
+    assert c["md5c"] == w["md5c"] + w["md5c_5"] + 1
+    assert c["rc4_ksa"] == w["rc4_ksa"] and c["rc4_prga_bytes"] == w["rc4_prga_byte"]
     c = _counts(oracle, streams, "pdf_testdoc_r2", "abcdefg")
     w = work.COUNTS["pdf_r2"]
     assert c["md5c"] == w["md5c"] and c["rc4_ksa"] == w["rc4_ksa"] and c["rc4_prga_bytes"] == w["rc4_prga_byte"]

@@ -3,7 +3,8 @@
 Usage: tools/prof_summary.py gpurun_out/prof_odt_r02 profiles/prof_odt_r02
 
 Counters are kept per --pmc pass (each pass is its own run of the program), averaged over the dispatches of
-each kernel, and the derived metrics are computed within one pass:
+each kernel (FETCH_SIZE / WRITE_SIZE: the median dispatch, see below), and the derived metrics are computed within
+one pass:
   valu_busy        = SQ_ACTIVE_INST_VALU * 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs)   (ROCm's VALUBusy formula,
                      derived_counters.xml; GRBM_GUI_ACTIVE is summed over the 8 XCDs on gfx950,
                      MI355X_MICROARCH.md)
@@ -87,9 +88,24 @@ def summarize(src, dst):
         per = {"per_dispatch": {}, "passes": {}}
         for sub, ctrs in passes.items():
             avg = {name: sum(v.values()) / len(v) for name, v in ctrs.items()}
+            # HBM byte counters: the MEDIAN dispatch (round 4).  A run's dispatches of one kernel move the same bytes
+            # except, in some runs, ONE dispatch that counts 2-3x (r03i: odt_e dispatch 4 269,946 KB vs 131,072 for the
+            # other three, R6 dispatch 7 260,698 vs 83,2xx KB): the mean made those read as 1.26x / 1.53x excess.  The
+            # per-dispatch values and the outliers are recorded.
+            for name in ("FETCH_SIZE", "WRITE_SIZE"):
+                if name in ctrs:
+                    vals = [ctrs[name][d] for d in sorted(ctrs[name], key=int)]
+                    med = sorted(vals)[len(vals) // 2] if len(vals) % 2 else sum(sorted(vals)[len(vals) // 2 - 1:len(vals) // 2 + 1]) / 2
+                    avg[name] = med
+                    per.setdefault("hbm_dispatch_values", {})[name] = vals
+                    out_d = [i for i, v in enumerate(vals) if med > 0 and v > 1.2 * med]
+                    if out_d:
+                        per.setdefault("hbm_outlier_dispatches", {})[name] = out_d
             ns = sum(dur[k][sub].values()) / max(1, len(dur[k][sub]))
             per["passes"][sub] = dict(avg, kernel_ns=ns, dispatches=len(dur[k][sub]))
-            per.setdefault("per_run_total", {}).update({name: sum(v.values()) for name, v in ctrs.items()})
+            per.setdefault("per_run_total", {}).update(
+                {name: (avg[name] * len(v) if name in ("FETCH_SIZE", "WRITE_SIZE") else sum(v.values()))
+                 for name, v in ctrs.items()})
             per["per_dispatch"].update(avg)
             g = avg.get("GRBM_GUI_ACTIVE")
             if g:
