@@ -153,23 +153,31 @@ DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc
         "=&v"(wn), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(h0)
 #define RC4_KSA_INS "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0)
 #define KB(q) "v"(kb[(q) % rc4_nkr<NK>::v])
+    /* A/B headers that merge with one v_perm (gen_rc4_ksa_asm.py --d16merge) read one more constant after the keys */
+#ifdef RC4_KSA_SELHIT
+    const uint32_t selhit = RC4_KSA_SELHIT, selno = RC4_KSA_SELNOHIT;
+#define RC4_KSA_XIN , "v"(selhit), "v"(selno)
+#else
+#define RC4_KSA_XIN
+#endif
     if constexpr (NK == 16) {
         asm volatile(RC4_KSA_ASM_16
                      : RC4_KSA_OUTS
                      : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9), KB(10),
-                       KB(11), KB(12), KB(13), KB(14), KB(15)
+                       KB(11), KB(12), KB(13), KB(14), KB(15) RC4_KSA_XIN
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     } else {
         /* the operand count is checked where the template is defined: the variant is chosen by the preprocessor */
         asm volatile(RC4_KSA_ASM_5
                      : RC4_KSA_OUTS
 #if RC4_KSA_NKR_5 == 10
-                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9)
+                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9) RC4_KSA_XIN
 #else
-                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4)
+                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4) RC4_KSA_XIN
 #endif
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     }
+#undef RC4_KSA_XIN
 #undef KB
 #undef RC4_KSA_INS
 #undef RC4_KSA_OUTS

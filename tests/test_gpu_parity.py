@@ -500,7 +500,11 @@ def test_calls_leave_the_callers_device_alone(dprf, streams):
     libamdhip64, which is what torch.cuda.current_device() reads).  With more than one GPU the caller sits on the LAST
     device and the context spans every device, so a call that moved it would be seen."""
     import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
+    dprf.lib()                                                       # libdprf.so pulls in the HIP runtime
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
     cur = ctypes.c_int(-1)
 
     def get():

@@ -57,6 +57,11 @@ def emulate(prog, keys, nk, sbase=0, text=None):
            "%19": 0x1010101010101010, "%20": np.uint64(0x03020100) + np.uint64(0x04040404) * (l4 >> np.uint64(6))}
     for q in range(nkr):
         vin["%%%d" % (21 + q)] = kb[q]
+    sel = re.search(r"#define RC4_KSA_SELHIT (0x[0-9a-f]+)u", text or "")
+    if sel:                                                # the --d16merge input after the key registers
+        vin["%%%d" % (21 + nkr)] = np.full(LANES, int(sel.group(1), 16), dtype=np.uint64)
+        no = re.search(r"#define RC4_KSA_SELNOHIT (0x[0-9a-f]+)u", text)
+        vin["%%%d" % (22 + nkr)] = np.full(LANES, int(no.group(1), 16), dtype=np.uint64)
     masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
     vcc = np.zeros(LANES, dtype=bool)
     M32 = np.uint64(0xffffffff)
@@ -119,8 +124,8 @@ def emulate(prog, keys, nk, sbase=0, text=None):
             assert "src0_sel:BYTE_0" in ln
             src1 = a[2].split()[0]
             if src1.startswith("%") and src1 not in sregs and (src1 not in vin or not isinstance(vin[src1], int)):
-                # a VGPR, byte-selected (BYTE_3 of j: the position counter)
-                sh1 = {"BYTE_0": 0, "BYTE_1": 8, "BYTE_3": 24}[re.search(r"src1_sel:(\w+)", ln).group(1)]
+                # a VGPR, byte-selected (BYTE_3 of j: the position counter; BYTE_2/3 of the ic4 constants)
+                sh1 = {"BYTE_0": 0, "BYTE_1": 8, "BYTE_2": 16, "BYTE_3": 24}[re.search(r"src1_sel:(\w+)", ln).group(1)]
                 r = (v(a[1]) & np.uint64(0xff)) == ((v(src1) >> np.uint64(sh1)) & np.uint64(0xff))
             else:
                 r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(src1))
@@ -130,6 +135,21 @@ def emulate(prog, keys, nk, sbase=0, text=None):
                 masks[a[0]] = r
         elif op == "ds_read_u8":
             regs[a[0]] = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
+        elif op in ("ds_read_u8_d16", "ds_read_u8_d16_hi"):
+            b = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
+            old = regs.get(a[0], np.zeros(LANES, dtype=np.uint64))
+            regs[a[0]] = (old & np.uint64(0xffff0000)) | b if op == "ds_read_u8_d16" else (old & np.uint64(0xffff)) | (b << np.uint64(16))
+        elif op == "v_perm_b32":
+            hi_, lo_, sel = v(a[1]), v(a[2]), v(a[3])
+            r = np.zeros(LANES, dtype=np.uint64)
+            for k in range(4):
+                sk = (sel >> np.uint64(8 * k)) & np.uint64(0xff)
+                src = np.where(sk >= 4, hi_, lo_)
+                byte = (src >> (np.uint64(8) * (sk & np.uint64(3)))) & np.uint64(0xff)
+                byte = np.where(sk == 0x0c, np.uint64(0), byte)
+                assert bool(np.all((sk <= 7) | (sk == 0x0c))), "selector values the emulator models: 0-7, 0x0c"
+                r |= byte << np.uint64(8 * k)
+            regs[a[0]] = r
         elif op == "ds_write_b8":
             lds[v(a[0]).astype(np.int64)] = (v(a[1]) & np.uint64(0xff)).astype(np.uint8)
         elif op == "ds_write_b128":
@@ -158,7 +178,7 @@ def emulate(prog, keys, nk, sbase=0, text=None):
             lds[ad] = (val & np.uint64(0xff)).astype(np.uint8)
             lds[ad + 1] = ((val >> np.uint64(8)) & np.uint64(0xff)).astype(np.uint8)
         elif op == "v_cndmask_b32_e32":
-            regs[a[0]] = np.where(vcc, v(a[2]), v(a[1]))
+            regs[a[0]] = np.where(vcc, v(a[2]), v(a[1]))     # src0 may be a literal (0x...)
         elif op == "v_cndmask_b32_sdwa":
             s0, s1 = v(a[1]), v(a[2])
             sel = {"DWORD": (0, 0xffffffff), "BYTE_0": (0, 0xff), "BYTE_1": (8, 0xff)}
@@ -199,14 +219,14 @@ def test_generated_ksa_equals_rc4(nk):
 
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1"])
+                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""
     import subprocess
     import sys
     gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen, flag], capture_output=True, text=True, check=True).stdout
+    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
     for nk in (5, 16):
         rng = random.Random(nk + 100)
         keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]

@@ -46,6 +46,9 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     above step 0's LDS pair, same instructions)
        tools/gen_rc4_ksa_asm.py --jctr > <variant header>         (A/B: i0 / i1 counted in byte 3 of j, key registers
                                                                     carrying the counter steps: 603 vs 612 M, slower)
+       tools/gen_rc4_ksa_asm.py --ic4 / --d16merge > <variant header>  (round 4 A/B: (i0, i1) of two groups in one
+                                                                    register, one v_add per two groups / x0, x1 by
+                                                                    d16 loads into one register, merged by one v_perm)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
                                                                     64-bit adds: 612 -> 595 M, the b128 stores cost
                                                                     more LDS time than the instructions they save)
@@ -65,7 +68,8 @@ def nkr_of(nk, jctr):
     return 10 if (jctr and nk % 2) else nk
 
 
-def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False):
+def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False, ic4=False,
+        d16=False):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -94,13 +98,33 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
     if jctr:
         vconst = False
     if vconst:
-        e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
+        i0f = 2 * FIRST_IC
+        # ic4 (round 4 A/B): (i0, i1) of two consecutive groups in bytes 0-3, bumped once per two groups
+        e("v_mov_b32 %s, 0x%x" % (IC, (i0f | ((i0f + 1) << 8) | ((i0f + 2) << 16) | ((i0f + 3) << 24)) if ic4
+                                  else (i0f | ((i0f + 1) << 8))))
+    # d16 (round 4 A/B): x0 / x1 land in the low / high half of ONE register (ds_read_u8_d16 / _d16_hi) and the
+    # merge is one v_perm whose selector is chosen by hit0 before the wait: SEL = hit0 ? [V1.b0, x0] : [x0, x1]
+    SEL = X1 if d16 else None                          # x1's register is free: both bytes land in X0
+    SEL_NOHIT, SEL_HIT = 0x0c0c0604, 0x0c0c0400        # v_perm(X, V1, sel): 4-7 = X bytes, 0-3 = V1 bytes
+    SELHIT = "%%%d" % (21 + nkr)                       # input VGPRs holding SEL_HIT, SEL_NOHIT (rc4_dev.h,
+    SELNO = "%%%d" % (22 + nkr)                        # RC4_KSA_SELHIT: VCC + a literal break the constant bus)
+
     def merge(q):
         """the deferred S[i0], S[i1] of group q as one u16 (VCC = hit0 of group q)"""
-        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
-        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-          % (M, X1, X0))
+        if d16:
+            e("v_perm_b32 %s, %s, %s, %s" % (M, X0, V1, SEL))
+        else:
+            e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+            e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
+              "src1_sel:DWORD" % (M, X1, X0))
         e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(2 * q)))
+
+    def icsel(k):
+        """SDWA byte of IC holding position i_k (k = 0, 1) of group q"""
+        return "BYTE_%d" % (k + (2 if (ic4 and (q - FIRST_IC) % 2) else 0))
+    RD0 = "ds_read_u8_d16" if d16 else "ds_read_u8"
+    RD1 = "ds_read_u8_d16_hi" if d16 else "ds_read_u8"
+    X1r = X0 if d16 else X1
 
     for q in range(128):
         i0, i1 = 2 * q, 2 * q + 1
@@ -127,8 +151,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             if q < FIRST_IC:
                 e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i1))
             else:
-                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_1" % (J, IC))
-            e("ds_read_u8 %s, %s" % (X0, A0))
+                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:%s" % (J, IC, icsel(1)))
+            e("%s %s, %s" % (RD0, X0, A0))
             e("ds_write_b8 %s, %s" % (A0, W))
         else:
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
@@ -152,14 +176,19 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             if q < FIRST_IC:
                 e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i0))
             else:
-                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:BYTE_0" % (J, IC))
-            e("ds_read_u8 %s, %s" % (X1, A1))
+                e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:%s" % (J, IC, icsel(0)))
+            e("%s %s, %s" % (RD1, X1r, A1))
         else:
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_read_u8 %s, %s" % (X1, A1))
         e("ds_write_b8 %s, %s" % (A1, V1))
+        if d16:             # two LDS instructions after the hit0 compare: the VCC read is hazard-free
+            e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (SEL, SELNO, SELHIT))
         if vconst and FIRST_IC <= q < 127:
-            e("v_add_u32 %s, 0x202, %s" % (IC, IC))
+            if not ic4:
+                e("v_add_u32 %s, 0x202, %s" % (IC, IC))
+            elif (q - FIRST_IC) % 2:
+                e("v_add_u32 %s, 0x4040404, %s" % (IC, IC))
         if late_merge:
             if q < 127:
                 e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
@@ -339,6 +368,8 @@ def main():
     pre = "--prefetch" in sys.argv
     vconst = "--salu-consts" not in sys.argv
     b128 = "--b128-identity" in sys.argv
+    ic4 = "--ic4" in sys.argv          # round 4 A/B: compare constants of two groups per register
+    d16 = "--d16merge" in sys.argv     # round 4 A/B: d16 loads + one v_perm merge
     # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
     # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
     jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
@@ -349,9 +380,12 @@ def main():
     print("   positions); 0 = the key byte in byte 0, anything above it.  RC4_KSA_NKR_5: registers of the 5-byte key */")
     print("#define RC4_KSA_KB_CTR %d" % (1 if jctr else 0))
     print("#define RC4_KSA_NKR_5 %d" % nkr_of(5, jctr))
+    if d16:
+        print("#define RC4_KSA_SELHIT 0x0c0c0400u   /* the block reads these two constants from the inputs after the keys */")
+        print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
         lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
-                 ksa(nk, early, late, pre, vconst and not early, b128, jctr))
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
