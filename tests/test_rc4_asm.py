@@ -219,7 +219,8 @@ def test_generated_ksa_equals_rc4(nk):
 
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge"])
+                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add",
+                                  "--split-add --ic4", "--split-add --ic4 --d16merge"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""

@@ -15,7 +15,7 @@ echo "== smoke $(date +%T)"
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { cat gpurun_out/smoke_$TAG.log; exit 1; }
 echo "== profile $(date +%T)"
 bash tools/profile_all.sh $TAG
-for W in odt office odt_e pdf_r34 pdf_r6 pdf_r2 pdf_r5; do
+for W in odt office odt_e pdf_r34 pdf_r3 pdf_r3_40 pdf_r6 pdf_r2 pdf_r5; do
   cp gpurun_out/summary_${W}_$TAG.json profiles/prof_${W}_$TAG.json
   cp gpurun_out/summary_${W}_${TAG}_kernel_stats.csv profiles/prof_${W}_${TAG}_kernel_stats.csv
 done

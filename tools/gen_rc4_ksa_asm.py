@@ -69,7 +69,7 @@ def nkr_of(nk, jctr):
 
 
 def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False, ic4=False,
-        d16=False):
+        d16=False, split=False):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -130,7 +130,12 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
         i0, i1 = 2 * q, 2 * q + 1
         if q > 0:
             e("s_waitcnt lgkmcnt(%d)" % (0 if late_merge else 1))
-        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nkr]))
+        # split (round 4 A/B): j + K is formed off the chain (into the address register that is free by then), so the
+        # chain pays one full-rate v_add after W / v1 arrives instead of a half-rate v_add3 -- same issue slots
+        if split and q > 0:
+            e("v_add_u32 %s, %s, %s" % (J, A1, W))
+        else:
+            e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nkr]))
         if not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i1))
         e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
@@ -158,9 +163,14 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:DWORD" % (J, ST))
             e("ds_read_u8 %s, %s" % (X0, A0))
             e("ds_write_b8 %s, %s" % (A0, W))
+        if split:           # M is free between merges (its last reader, the previous u16 store, is long issued)
+            e("v_add_u32 %s, %s, %s" % (M, J, KB[i1 % nkr]))
         e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
           % (V1, W, W))
-        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nkr]))
+        if split:
+            e("v_add_u32 %s, %s, %s" % (J, M, V1))
+        else:
+            e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nkr]))
         if not early_read and not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i0))
         e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
@@ -202,6 +212,8 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
         else:
             e("s_waitcnt lgkmcnt(0)")
         merge(q)
+        if split and q < 127:   # the next group's j + K, off the chain (A1's last reader is several issues back)
+            e("v_add_u32 %s, %s, %s" % (A1, J, KB[(i0 + 2) % nkr]))
     e("s_waitcnt lgkmcnt(0)")
     return out
 
@@ -370,6 +382,7 @@ def main():
     b128 = "--b128-identity" in sys.argv
     ic4 = "--ic4" in sys.argv          # round 4 A/B: compare constants of two groups per register
     d16 = "--d16merge" in sys.argv     # round 4 A/B: d16 loads + one v_perm merge
+    split = "--split-add" in sys.argv  # round 4 A/B: j + K off the chain, one full-rate v_add on it
     # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
     # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
     jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
@@ -385,7 +398,7 @@ def main():
         print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
         lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
-                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16))
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)

@@ -15,7 +15,8 @@ import sys
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CUS, XCDS = 256, 8
 DOM = {"odt": "k_odt_kdf", "odt_e": "k_odt_kdf", "office": "k_office_kdf", "pdf_r34": "k_pdf_r24",
-       "pdf_r2": "k_pdf_r24", "pdf_r5": "k_pdf_r5", "pdf_r6": "k_pdf_r6"}
+       "pdf_r3": "k_pdf_r24", "pdf_r3_40": "k_pdf_r24", "pdf_r2": "k_pdf_r24", "pdf_r5": "k_pdf_r5",
+       "pdf_r6": "k_pdf_r6"}
 tags = sys.argv[1:] or ["r02"]
 traffic, valu = {}, {}
 for w, kname in DOM.items():
