@@ -762,10 +762,82 @@ DEVI void r6_push(r6_shared *sh, const r6_lds &S, uint32_t slot) {
 }
 
 
+/* Reserving claims (round 4 A/B, R6_RESERVE): the claim above reads the class counts as a hint and decrements after it
+ * has taken its bits, so two waves that pick the same class at the same time split its slots -- one of them then runs a
+ * whole round (~10^5 issue slots) for a handful of lanes.  Here lane 0 first RESERVES min(count, 64) slots of the class
+ * with a compare-and-swap on its count, and the wave then takes exactly that many bits, scanning again if a racing wave
+ * took bits it had chosen.  Termination: a push sets its bit before it increments the count and a claim decrements the
+ * count before it clears bits, so at every moment the set bits are at least the count, and every reservation (made
+ * against the count) has its bits. */
+#ifndef R6_RESERVE
+#define R6_RESERVE 0
+#endif
+#ifndef R6_RESERVE_PASSES
+#define R6_RESERVE_PASSES 2
+#endif
+#if R6_RESERVE
+DEVI uint32_t r6_claim_reserved(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t best) {
+    uint32_t k = 0;
+    if (lane == 0) {
+        uint32_t old = lds_load(&sh->count[best]);
+        while (old > 0u) {
+            const uint32_t want = old < 64u ? old : 64u;
+            const uint32_t seen = atomicCAS(&sh->count[best], old, old - want);
+            if (seen == old) { k = want; break; }
+            old = seen;
+        }
+    }
+    k = __builtin_amdgcn_readlane(k, 0);
+    if (k == 0u) return 0;
+    /* one pass over the bitmap for the k reserved slots, then (R6_RESERVE_PASSES 2) a second one for what a racing
+     * wave took first; a reservation still unfilled after that is given back to the count */
+    uint32_t total = 0;
+#pragma unroll
+    for (int pass = 0; pass < R6_RESERVE_PASSES; pass++) {
+        if (total >= k) break;                           /* uniform */
+        const uint32_t need = k - total;
+        const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
+        const uint32_t pc = __builtin_popcount(w);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if (lane >= (uint32_t)d) inc += o;
+        }
+        uint32_t take = 0u;
+        if (inc <= need) {
+            take = w;
+        } else if (inc - pc < need) {
+            for (uint32_t q = need - (inc - pc), rest = w; q; q--) {
+                take |= rest & (0u - rest);
+                rest &= rest - 1u;
+            }
+        }
+        const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
+        const uint32_t ng = __builtin_popcount(got);
+        uint32_t off = ng;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(off, d, 64);
+            if (lane >= (uint32_t)d) off += o;
+        }
+        const uint32_t pass_total = __builtin_amdgcn_readlane(off, 63);
+        off = total + off - ng;
+        for (uint32_t b = got; b; b &= b - 1u) sh->stage[wave][off++] = (uint16_t)(lane * 32u + __builtin_ctz(b));
+        total += pass_total;
+    }
+    if (lane == 0 && total < k) atomicAdd(&sh->count[best], k - total);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
+    *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
+    return total;
+}
+#endif
+
 /* Wave-uniform: claim up to 64 queued slots of the fullest class; returns how many (0: none queued) and
  * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
  * order up to 64 in total, clear exactly the bits they chose (atomicAnd returns what they got when another
  * wave raced them), and the ids are handed out through the wave's stage row. */
+template <int MODE>
 DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t *queue) {
     const uint32_t cnt = lane < R6_QUEUES ? lds_load(&sh->count[lane]) : 0u;
     uint32_t best = R6_CLASSES, bc = 0;
@@ -782,6 +854,10 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
 #endif
     *queue = best;
     if (bc == 0) return 0;
+#if R6_RESERVE
+    /* range mode only: the list-mode instantiations spill 12 B/lane with it at the 168-VGPR limit */
+    if (MODE == 0 && best < R6_CLASSES) return r6_claim_reserved(sh, lane, wave, slot, best);
+#endif
     const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
     const uint32_t pc = __builtin_popcount(w);
     /* inclusive scan of the word popcounts over the wave */
@@ -880,7 +956,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
     if (lane == 0) sh->idle_t0[wave] = 0ull;
     for (;;) {
         uint32_t slot, queue;
-        const uint32_t n = r6_claim(sh, opaque_lane(), wave, &slot, &queue);
+        const uint32_t n = r6_claim<MODE>(sh, opaque_lane(), wave, &slot, &queue);
         if (n == 0) {
             if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
             /* watchdog on the constant-rate wall clock: a wave that has found nothing queued for idle_ticks
