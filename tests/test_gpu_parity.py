@@ -475,7 +475,7 @@ def test_list_status_marks_only_the_invalid_candidates(dprf, streams):
 
 
 @pytest.mark.parametrize("name,length,skipped", [("odt_long_e_200", 200, 0), ("pdf_r6_long176", 176, 0),
-                                                 ("pdf_r6_long176", 200, 1)])
+                                                 ("pdf_r6_long176", 176, 1)])
 def test_gpu_client_verifies_long_payloads(dprf, long_verdicts, name, length, skipped):
     """the GPU client drops no candidate the reference verifies -- a payload of 200-byte ODF candidates
     (and 176-byte R6 ones) is verified whole, the document's password among them is found.  Only what the reference
