@@ -37,7 +37,7 @@ WORKLOADS = {
                "configs[0]: ECMA-376 Standard Encryption (password.docx), -pr 4 lowercase"),
     "pdf_r34": ("pdf_testdoc_r4", ALNUM, 7, 1 << 28, "pdf_r34",
                 "configs[2]: PDF 1.7 V4/R4 (password_1.7_v4_r4.pdf), MD5 x50 + RC4 x20, -pr 7 alnum"),
-    "pdf_r6": ("pdf_synth_r6_ox", LOWER, 6, 1 << 24, "pdf_r6",
+    "pdf_r6": ("pdf_synth_r6_ox", LOWER, 6, 1 << 25, "pdf_r6",   # 2^25: one ~9 s launch per step
                "configs[3]: PDF 2.0 R6 hardened hash (synthetic document), -pr 6 lowercase"),
     "pdf_r2": ("pdf_testdoc_r2", ALNUM, 7, 1 << 30, "pdf_r2", "PDF 1.3 V1/R2 (password_1.3_v1_r2.pdf), -pr 7 alnum"),
     "pdf_r5": ("pdf_synth_r5_cat", ALNUM, 7, 1 << 31, "pdf_r5", "PDF R5 (synthetic document), -pr 7 alnum"),
