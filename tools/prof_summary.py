@@ -88,10 +88,11 @@ def summarize(src, dst):
         per = {"per_dispatch": {}, "passes": {}}
         for sub, ctrs in passes.items():
             avg = {name: sum(v.values()) / len(v) for name, v in ctrs.items()}
-            # HBM byte counters: the MEDIAN dispatch (round 4).  A run's dispatches of one kernel move the same bytes
-            # except, in some runs, ONE dispatch that counts 2-3x (r03i: odt_e dispatch 4 269,946 KB vs 131,072 for the
-            # other three, R6 dispatch 7 260,698 vs 83,2xx KB): the mean made those read as 1.26x / 1.53x excess.  The
-            # per-dispatch values and the outliers are recorded.
+            # HBM byte counters (round 4): every dispatch's value is recorded, and per_dispatch holds the MEDIAN dispatch
+            # (round 3's r03i profiles had one dispatch at 2-3x the others -- odt_e 269,946 vs 131,072 KiB, R6 260,698 vs
+            # 83,2xx KiB -- which a re-check over 16 + 10 dispatches did not reproduce: profiles/write_size_recheck_r04b.json).
+            # Bytes per CANDIDATE stay total / candidates of the run: R6's launches differ in size within a run (2^22 until
+            # the rate is measured, then ~2^25), where a median dispatch says nothing per candidate.
             for name in ("FETCH_SIZE", "WRITE_SIZE"):
                 if name in ctrs:
                     vals = [ctrs[name][d] for d in sorted(ctrs[name], key=int)]
@@ -103,9 +104,7 @@ def summarize(src, dst):
                         per.setdefault("hbm_outlier_dispatches", {})[name] = out_d
             ns = sum(dur[k][sub].values()) / max(1, len(dur[k][sub]))
             per["passes"][sub] = dict(avg, kernel_ns=ns, dispatches=len(dur[k][sub]))
-            per.setdefault("per_run_total", {}).update(
-                {name: (avg[name] * len(v) if name in ("FETCH_SIZE", "WRITE_SIZE") else sum(v.values()))
-                 for name, v in ctrs.items()})
+            per.setdefault("per_run_total", {}).update({name: sum(v.values()) for name, v in ctrs.items()})
             per["per_dispatch"].update(avg)
             g = avg.get("GRBM_GUI_ACTIVE")
             if g:
