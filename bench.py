@@ -459,8 +459,11 @@ def main():
                           "pwlen": spl, "bound": measured_bound(pmc_summary(name, build), skey)[0],
                           "steps": args.side_steps, "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
                           "dominant_avg_ms": sm["avg_launch_ms"], "candidates_per_launch": sm["per_launch"],
-                          "valu_floor_frac": (sm["per_launch"] * work.per_candidate(skey)
-                                              / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak),
+                          # the larger of the launch-time and the wall-time figure: R2-R4 launches overlap on two
+                          # streams (a launch's event time then includes its neighbour's), other formats' do not
+                          "valu_floor_frac": max(sm["per_launch"] * work.per_candidate(skey)
+                                                 / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak,
+                                                 sm["value"] / world / max(1, len(devices)) * work.per_candidate(skey) / peak),
                           "call_overhead": sm["call_overhead"]}
             if skey in work.LDS_CYCLES:             # RC4 formats: the modelled LDS-array share (~ rocprof LdsUtil)
                 side[name]["lds_cycle_frac"] = work.lds_frac(

@@ -48,7 +48,7 @@ int main() {
     const int nblk = 256 * 24;
     unsigned long long *drec; int *sink;
     CHECK(hipMalloc(&drec, 3 * 8 * nblk)); CHECK(hipMalloc(&sink, 4));
-    probe<16384>(nblk, drec, sink); probe<16128>(nblk, drec, sink); probe<15872>(nblk, drec, sink);
+    probe<16384>(nblk, drec, sink); probe<16256>(nblk, drec, sink); probe<16208>(nblk, drec, sink); probe<16128>(nblk, drec, sink); probe<16000>(nblk, drec, sink); probe<15872>(nblk, drec, sink);
     probe<15360>(nblk, drec, sink); probe<14848>(nblk, drec, sink); probe<13312>(nblk, drec, sink);
     probe<8192>(nblk, drec, sink); probe<1024>(nblk, drec, sink);
     return 0;
