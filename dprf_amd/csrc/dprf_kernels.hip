@@ -793,9 +793,11 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
  * Batches per workgroup, R3/R4: 2 / 4 / 8 = 472 / 480 / 481 M (G = 4), 6 / 8 / 12 = 513 / 513 / 507 M (G = 2);
  * R2: 8 / 16 / 24 = 9.58 / 9.68 / 9.70 G.  Re-measured on the group-deferred KSA: R3/R4 6 / 8 / 12 batches
  * 559 / 560 / 557 M, priority 0 / 1 / 3 529 / 560 / 560 M; R2 8 / 16 / 24 batches 11.08 / 11.25 / 11.32 G,
- * priority 0 10.56 G. */
+ * priority 0 10.56 G.  Round 3 (asm KSA): 8 / 12 / 16 = 613 / 608 / 603 M; round 4, with consecutive launches on two
+ * streams (the last partial generation of one launch overlaps the next): 8 / 12 / 16 = 626.2 / 628.5 / 625.2 M (three
+ * alternating runs each, every run of 12 above the neighbouring 8), so 12. */
 #ifndef R34_BATCHES
-#define R34_BATCHES 8
+#define R34_BATCHES 12
 #endif
 #ifndef R2_BATCHES
 #define R2_BATCHES 24

@@ -85,6 +85,14 @@ DEVI lds_u8 *L8(uint32_t a) { return (lds_u8 *)(size_t)a; }
 DEVI lds_u32 *L32(uint32_t a) { return (lds_u32 *)(size_t)a; }
 DEVI uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(const lds_u8 *)p; }
 
+/* the lane index as an opaque value (LLVM cannot hoist it): used where a lane-derived value would otherwise be held
+ * across the persistent loop -- at the kernel's VGPR limit such values were what the register allocator spilled */
+DEVI uint32_t opaque_lane() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 struct r6_lds {
     uint32_t pat;              /* LDS byte address of the slot's group: rows of 256 bytes */
     uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
@@ -526,7 +534,13 @@ template <bool UNI>
 DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16], uint32_t colbytes) {
     uint32_t Lp = len + bs;
     if (UNI) Lp = __builtin_amdgcn_readfirstlane(Lp);
+#if R6_PROBE_LANECOL
+    /* timing / PMC probe only (wrong results): the blocks are read from the column of the LANE's index instead of the
+     * slot's, so a 32-lane half meets 32 banks -- what the period-column bank conflicts cost */
+    const uint32_t colbase = UNI ? S.pat + ((opaque_lane() & 63u) << 2) : S.pat + S.lanebase;
+#else
     const uint32_t colbase = S.pat + S.lanebase;                 /* pat is only 16-byte aligned */
+#endif
     r6_load_k(S, len, K);
     /* AES-128 key K[0:16], iv K[16:32] (:259-261) */
     uint32_t rk[44];
@@ -697,14 +711,6 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
     S.base = c4 + (gb ? 0x00c08040u : 0xc0804000u);
 #endif
     return S;
-}
-
-/* the lane index as an opaque value (LLVM cannot hoist it): used where a lane-derived value would otherwise be held
- * across the persistent loop -- at the kernel's VGPR limit such values were what the register allocator spilled */
-DEVI uint32_t opaque_lane() {
-    uint32_t l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
 }
 
 DEVI uint32_t lds_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
