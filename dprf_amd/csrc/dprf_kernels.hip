@@ -795,12 +795,13 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
  * 559 / 560 / 557 M, priority 0 / 1 / 3 529 / 560 / 560 M; R2 8 / 16 / 24 batches 11.08 / 11.25 / 11.32 G,
  * priority 0 10.56 G.  Round 3 (asm KSA): 8 / 12 / 16 = 613 / 608 / 603 M; round 4, with consecutive launches on two
  * streams (the last partial generation of one launch overlaps the next): 8 / 12 / 16 = 626.2 / 628.5 / 625.2 M (three
- * alternating runs each, every run of 12 above the neighbouring 8), so 12. */
+ * alternating runs each, every run of 12 above the neighbouring 8), so 12.  R2 likewise: 16 / 24 / 36 / 48 = 12.23 /
+ * 12.27 / 12.32 / 12.31 G, so 36 (profiles/ab_r2_batches_r04l.txt). */
 #ifndef R34_BATCHES
 #define R34_BATCHES 12
 #endif
 #ifndef R2_BATCHES
-#define R2_BATCHES 24
+#define R2_BATCHES 36
 #endif
 #ifndef R24_PRIO
 #define R24_PRIO 3
