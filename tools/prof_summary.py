@@ -91,8 +91,8 @@ def summarize(src, dst):
             # HBM byte counters (round 4): every dispatch's value is recorded, and per_dispatch holds the MEDIAN dispatch
             # (round 3's r03i profiles had one dispatch at 2-3x the others -- odt_e 269,946 vs 131,072 KiB, R6 260,698 vs
             # 83,2xx KiB -- which a re-check over 16 + 10 dispatches did not reproduce: profiles/write_size_recheck_r04b.json).
-            # Bytes per CANDIDATE stay total / candidates of the run: R6's launches differ in size within a run (2^22 until
-            # the rate is measured, then ~2^25), where a median dispatch says nothing per candidate.
+            # Bytes per CANDIDATE: below (per dispatch, by duration share -- R6's launches differ in size within a run, 2^22
+            # until the rate is measured, then ~2^25, where a median dispatch says nothing per candidate).
             for name in ("FETCH_SIZE", "WRITE_SIZE"):
                 if name in ctrs:
                     vals = [ctrs[name][d] for d in sorted(ctrs[name], key=int)]
@@ -140,8 +140,25 @@ def summarize(src, dst):
             if batch:
                 tot = per["per_run_total"]
                 per["pmc_candidates"] = batch * PMC_STEPS
-                per["hbm_bytes_per_candidate"] = (tot.get("FETCH_SIZE", 0) + tot.get("WRITE_SIZE", 0)) * 1024 / (
+                per["hbm_bytes_per_candidate_run_total"] = (tot.get("FETCH_SIZE", 0) + tot.get("WRITE_SIZE", 0)) * 1024 / (
                     batch * PMC_STEPS)
+                # per candidate: the median over dispatches of bytes / that dispatch's candidates, which are estimated as the
+                # run's candidates in proportion to the dispatch's duration (one kernel at a steady rate; the launch sizes
+                # of a run differ).  The run total alone let one first dispatch that wrote 2-3x the others (r03i, r04m: R6
+                # 260,5xx vs 83,2xx KiB at equal size) decide the figure.
+                bpc = 0.0
+                for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+                    vals = passes.get(sub, {}).get(name)
+                    ds = dur[k].get(sub, {})
+                    tdur = sum(ds.get(d, 0) for d in (vals or {}))
+                    if not vals or not tdur:
+                        continue
+                    pcs = sorted(v * 1024 / (batch * PMC_STEPS * ds[d] / tdur) for d, v in vals.items() if ds.get(d))
+                    m = len(pcs)
+                    med = pcs[m // 2] if m % 2 else (pcs[m // 2 - 1] + pcs[m // 2]) / 2
+                    per.setdefault("hbm_bytes_per_candidate_by_dispatch", {})[name] = pcs
+                    bpc += med
+                per["hbm_bytes_per_candidate"] = bpc
         summ[k] = per
     out["counters"] = summ
     json.dump(out, open(dst + ".json", "w"), indent=1)
