@@ -87,6 +87,48 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
             if (OP == 50) asm volatile("v_cmp_eq_u32_sdwa vcc, %0, %1 src0_sel:BYTE_0 src1_sel:DWORD\n\ts_nop 1\n\tv_cndmask_b32_e32 %0, %0, %2, vcc" : "+v"(x[c]) : "v"(y), "v"(z) : "vcc");
             if (OP == 51) asm volatile("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0" : "+v"(x[c]) : "v"(y));
             if (OP == 52) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "+v"(x[c]) : "v"(y));
+            if (OP == 53) { /* the SHA-1 instruction mix of the ODF / Office KDF loops (round 4): per 8 instructions 3
+                               alignbit, 2 add3, 2 bitop3, 1 xor -- 14.4 issue slots by the cost table of work.py */
+                asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_add3_u32 %0, %0, %1, %2\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
+                             "v_add3_u32 %0, %0, %2, %1\n\tv_xor_b32 %0, %0, %1\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 31\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8"
+                             : "+v"(x[c]) : "v"(y), "v"(z));
+            }
+            if (OP == 54) { /* the same eight as four interleaved pairs of the alignbit / add3 / bitop3 / xor streams */
+                if (c & 1) asm volatile("v_add3_u32 %0, %0, %1, %2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
+                                        "v_xor_b32 %0, %0, %1\n\tv_alignbit_b32 %0, %0, %0, 5" : "+v"(x[c]) : "v"(y), "v"(z));
+                else asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_add3_u32 %0, %0, %1, %2\n\t"
+                                  "v_alignbit_b32 %0, %0, %0, 2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
+            }
+            if (OP == 55) { /* the mix as separate statements: the compiler interleaves the eight chains */
+                asm volatile("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
+                asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm volatile("v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm volatile("v_add3_u32 %0, %0, %2, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                asm volatile("v_alignbit_b32 %0, %0, %0, 31" : "+v"(x[c]));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
+            }
+            if (OP == 56) asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 57) asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 58) asm volatile("v_add3_u32 %0, %0, %1, %2\n\tv_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 59) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 60) { if (c & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                            else asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z)); }
+            if (OP == 61) asm volatile("v_add3_u32 %0, %0, %1, %2\n\tv_add_u32 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 62) asm volatile("v_xor_b32 %0, %0, %1\n\tv_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 63) asm volatile("v_add3_u32 %0, %0, %1, %2\n\tv_xor_b32_e64 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 64) asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+            if (OP == 65) { if (c & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                            else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z)); }
+            if (OP == 66) { if (c & 1) asm volatile("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
+                            else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z)); }
+            if (OP == 67) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_bitop3_b32 %0, %0, %2, %1 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
+            if (OP == 68) { unsigned t = x[c]; /* bitop3 with 16 independent chains (two per x) */
+                asm volatile("v_bitop3_b32 %0, %0, %2, %3 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %3, %2 bitop3:0x96" : "+v"(x[c]), "+v"(t) : "v"(y), "v"(z));
+                x[c] ^= t; }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -124,8 +166,30 @@ double run(const char *name, int blocks, int per_iter) {
     return rate;
 }
 
-int main() {
+int main(int argc, char **argv) {
     const int blocks = 32768;
+    if (argc > 1) {   /* "mix": the KDF instruction mix against the additive slot model (78.64 T x 8 / 14.4) */
+        run<53>("sha1 mix x8", blocks, 8);
+        run<54>("sha1 mix x4 il", blocks, 4);
+        run<55>("sha1 mix stmts", blocks, 8);
+        run<56>("alignbit+add3", blocks, 2);
+        run<57>("alignbit+bitop3", blocks, 2);
+        run<58>("add3+xor", blocks, 2);
+        run<59>("bitop3+xor", blocks, 2);
+        run<60>("add3|xor indep", blocks, 1);
+        run<61>("add3>add dep", blocks, 2);
+        run<62>("xor>add3 dep", blocks, 2);
+        run<63>("add3>xor_e64 dep", blocks, 2);
+        run<64>("alignbit>xor dep", blocks, 2);
+        run<65>("bitop3|xor indep", blocks, 1);
+        run<66>("alignbit|bitop3 indep", blocks, 1);
+        run<67>("bitop3>bitop3 dep", blocks, 2);
+        run<2>("v_alignbit_b32", blocks, 1);
+        run<0>("v_add3_u32", blocks, 1);
+        run<1>("v_bitop3_b32", blocks, 1);
+        printf("slot model for the mix: %.2f T lane-instr/s\n", 78.6432 * 8 / 14.4);
+        return 0;
+    }
     run<3>("v_xor_b32", blocks, 1);
     run<31>("v_cndmask vcc", blocks, 1);
     run<47>("v_cndmask e64 s", blocks, 1);
