@@ -115,6 +115,15 @@ def emulate(prog, keys, nk, sbase=0, text=None):
             regs[a[0]] = (v(a[1]) + v(a[2]) + v(a[3])) & M32
         elif op == "v_and_or_b32":
             regs[a[0]] = (v(a[1]) & v(a[2])) | v(a[3])
+        elif op == "v_bitop3_b32":
+            lut = int(re.search(r"bitop3:(0x[0-9a-f]+)", ln).group(1), 16)
+            x0, x1, x2 = v(a[1]), v(a[2]), v(a[3].split()[0])
+            r = np.zeros(LANES, dtype=np.uint64)
+            for b in range(32):
+                idx = (((x0 >> np.uint64(b)) & np.uint64(1)) << np.uint64(2)) | (((x1 >> np.uint64(b)) & np.uint64(1)) << np.uint64(1)) \
+                    | ((x2 >> np.uint64(b)) & np.uint64(1))
+                r |= ((np.uint64(lut) >> idx) & np.uint64(1)) << np.uint64(b)
+            regs[a[0]] = r
         elif op == "v_lshrrev_b32_sdwa":
             assert "dst_sel:BYTE_1" in ln and "UNUSED_PRESERVE" in ln and "src1_sel:BYTE_0" in ln
             src = v(a[2].split()[0]) & np.uint64(0xff)
@@ -220,7 +229,7 @@ def test_generated_ksa_equals_rc4(nk):
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
                                   "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add",
-                                  "--split-add --ic4", "--split-add --ic4 --d16merge"])
+                                  "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""

@@ -16,7 +16,7 @@ of 131 instructions per KSA) lost 3 %.  The schedule is rc4_ksa's group-deferred
     wait for W = S[i0] | S[i1] << 8            (read at the end of group q - 1; lgkmcnt(1): the u16 store
                                                  issued after it may stay in flight -- LDS completes in order)
     j += W + K[i0]                              (only j's low byte is ever used: W's byte 1 above it is harmless)
-    a0 = (j & 3) | lanebase; a0.byte1 = j.byte0 >> 2            -> address of S[j] in the [i/4][lane][i%4] layout
+    a0 = (j & 3) | lanebase (v_bitop3); a0.byte1 = j.byte0 >> 2  -> address of S[j] in the [i/4][lane][i%4] layout
     hit1 = (j.byte0 == i1)                      (i1 an inline constant while <= 64, else byte 1 of a VGPR (i0, i1)
                                                  bumped by 0x0202 once per group: no SALU in the loop)
     x0 = S[j]; S[j] = W.byte0
@@ -49,6 +49,8 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
        tools/gen_rc4_ksa_asm.py --ic4 / --d16merge > <variant header>  (round 4 A/B: (i0, i1) of two groups in one
                                                                     register, one v_add per two groups / x0, x1 by
                                                                     d16 loads into one register, merged by one v_perm)
+       tools/gen_rc4_ksa_asm.py --and-or > <variant header>        (the S[j] address's low byte by v_and_or_b32, half
+                                                                    rate, as before round 4; default: v_bitop3_b32)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
                                                                     64-bit adds: 612 -> 595 M, the b128 stores cost
                                                                     more LDS time than the instructions they save)
@@ -69,7 +71,7 @@ def nkr_of(nk, jctr):
 
 
 def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False, ic4=False,
-        d16=False, split=False):
+        d16=False, split=False, b3addr=False):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -138,7 +140,7 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nkr]))
         if not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i1))
-        e("v_and_or_b32 %s, %s, 3, %s" % (A0, J, LB))
+        e(addr_lo(A0, J, LB, b3addr))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
           % (A0, J))
         if late_merge and q > 0:
@@ -173,7 +175,7 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nkr]))
         if not early_read and not vconst and not jctr:
             e("s_movk_i32 %s, %d" % (ST, i0))
-        e("v_and_or_b32 %s, %s, 3, %s" % (A1, J, LB))
+        e(addr_lo(A1, J, LB, b3addr))
         e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
           % (A1, J))
         if early_read:
@@ -216,6 +218,14 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
             e("v_add_u32 %s, %s, %s" % (A1, J, KB[(i0 + 2) % nkr]))
     e("s_waitcnt lgkmcnt(0)")
     return out
+
+
+def addr_lo(A, J, LB, b3addr):
+    """A = (j & 3) | lanebase.  b3addr (round 4): as v_bitop3_b32 (LUT 0xea = (s0 & s1) | s2), which issues at full rate
+    on gfx950 unless its three sources share a VGPR bank (profiles/vgpr_bank_r04.txt), where v_and_or_b32 is half rate"""
+    if b3addr:
+        return "v_bitop3_b32 %s, %s, 3, %s bitop3:0xea" % (A, J, LB)
+    return "v_and_or_b32 %s, %s, 3, %s" % (A, J, LB)
 
 
 def ksa_early_v1(nk):
@@ -383,6 +393,9 @@ def main():
     ic4 = "--ic4" in sys.argv          # round 4 A/B: compare constants of two groups per register
     d16 = "--d16merge" in sys.argv     # round 4 A/B: d16 loads + one v_perm merge
     split = "--split-add" in sys.argv  # round 4 A/B: j + K off the chain, one full-rate v_add on it
+    # the address's low byte by v_bitop3 (full rate) instead of v_and_or (half rate): default since round 4 (R3/R4 625.7
+    # -> 628.3 M, R2 12.38 -> 12.39 G, profiles/ab_r24_b3addr_r04n.txt); --and-or restores the old form
+    b3addr = "--and-or" not in sys.argv
     # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
     # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
     jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
@@ -398,7 +411,7 @@ def main():
         print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
         lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
-                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split))
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
