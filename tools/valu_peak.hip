@@ -129,6 +129,43 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
             if (OP == 68) { unsigned t = x[c]; /* bitop3 with 16 independent chains (two per x) */
                 asm volatile("v_bitop3_b32 %0, %0, %2, %3 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %3, %2 bitop3:0x96" : "+v"(x[c]), "+v"(t) : "v"(y), "v"(z));
                 x[c] ^= t; }
+            /* half-rate (add3) / full-rate (xor) patterns over the eight independent chains (round 4) */
+            if (OP == 70) { if ((c >> 1) & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                            else asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z)); }   /* HHFFHHFF */
+            if (OP == 71) { if (c >= 4) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                            else asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z)); }   /* HHHHFFFF */
+            if (OP == 72) { if (c == 7) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
+                            else asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z)); }   /* 7H 1F */
+            if (OP == 73) { if (c == 7) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                            else asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y)); }               /* 7F 1H */
+            if (OP == 74) { if (c & 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
+                            else asm volatile("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c])); }                /* H F (bitop3) */
+            /* round 4: the ODF KDF loop's instruction counts per 2 PBKDF2 iterations (887 alignbit, 566 add3, 516 bitop3,
+             * 268 xor, 110 add) as a 21-instruction pattern per chain, and the same work with every add3 as two v_add
+             * (26 instructions, 30 % half-rate instead of 62 %) */
+            if (OP == 80) {
+                asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
+                             "v_add3_u32 %0, %0, %1, %2\n\tv_alignbit_b32 %0, %0, %0, 2\n\tv_add3_u32 %0, %0, %2, %1\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_alignbit_b32 %0, %0, %0, 31\n\t"
+                             "v_xor_b32 %0, %0, %1\n\tv_add3_u32 %0, %0, %1, %2\n\tv_alignbit_b32 %0, %0, %0, 5\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8\n\tv_add3_u32 %0, %0, %2, %1\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 30\n\tv_add_u32 %0, %0, %1\n\tv_alignbit_b32 %0, %0, %0, 1\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_add3_u32 %0, %0, %1, %2\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 27\n\tv_xor_b32 %0, %0, %2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]) : "v"(y), "v"(z));
+            }
+            if (OP == 81) {
+                asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
+                             "v_add_u32 %0, %0, %1\n\tv_add_u32 %0, %0, %2\n\tv_alignbit_b32 %0, %0, %0, 2\n\t"
+                             "v_add_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_alignbit_b32 %0, %0, %0, 31\n\t"
+                             "v_xor_b32 %0, %0, %1\n\tv_add_u32 %0, %0, %1\n\tv_add_u32 %0, %0, %2\n\tv_alignbit_b32 %0, %0, %0, 5\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8\n\tv_add_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 30\n\tv_add_u32 %0, %0, %1\n\tv_alignbit_b32 %0, %0, %0, 1\n\t"
+                             "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\tv_add_u32 %0, %0, %1\n\tv_add_u32 %0, %0, %2\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 27\n\tv_xor_b32 %0, %0, %2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
+                             "v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]) : "v"(y), "v"(z));
+            }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -184,6 +221,14 @@ int main(int argc, char **argv) {
         run<65>("bitop3|xor indep", blocks, 1);
         run<66>("alignbit|bitop3 indep", blocks, 1);
         run<67>("bitop3>bitop3 dep", blocks, 2);
+        run<70>("HHFF x2 indep", blocks, 1);
+        run<71>("HHHHFFFF indep", blocks, 1);
+        run<72>("7H 1F indep", blocks, 1);
+        run<73>("7F 1H indep", blocks, 1);
+        run<74>("alignbit|bitop3 alt", blocks, 1);
+        run<80>("odf mix (21, add3)", blocks, 21);
+        run<81>("odf mix (26, add3 as 2 add)", blocks, 26);
+        printf("per 21-instruction unit of work: cycles = 21 x 157.29 T / rate(80) vs 26 x 157.29 T / rate(81)\n");
         run<2>("v_alignbit_b32", blocks, 1);
         run<0>("v_add3_u32", blocks, 1);
         run<1>("v_bitop3_b32", blocks, 1);
