@@ -166,6 +166,29 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
                              "v_alignbit_b32 %0, %0, %0, 27\n\tv_xor_b32 %0, %0, %2\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
                              "v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]) : "v"(y), "v"(z));
             }
+            if (OP == 82) { /* the 21-instruction ODF pattern as separate statements: the compiler interleaves the chains */
+                asm("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
+                asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]));
+                asm("v_add3_u32 %0, %0, %2, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 31" : "+v"(x[c]));
+                asm("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 5" : "+v"(x[c]));
+                asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_add3_u32 %0, %0, %2, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 30" : "+v"(x[c]));
+                asm("v_add_u32 %0, %0, %1" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 1" : "+v"(x[c]));
+                asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 27" : "+v"(x[c]));
+                asm("v_xor_b32 %0, %0, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(x[c]) : "v"(y), "v"(z));
+                asm("v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]));
+            }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -228,6 +251,7 @@ int main(int argc, char **argv) {
         run<74>("alignbit|bitop3 alt", blocks, 1);
         run<80>("odf mix (21, add3)", blocks, 21);
         run<81>("odf mix (26, add3 as 2 add)", blocks, 26);
+        run<82>("odf mix (21) chains interleaved", blocks, 21);
         printf("per 21-instruction unit of work: cycles = 21 x 157.29 T / rate(80) vs 26 x 157.29 T / rate(81)\n");
         run<2>("v_alignbit_b32", blocks, 1);
         run<0>("v_add3_u32", blocks, 1);
