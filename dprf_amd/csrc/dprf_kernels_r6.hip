@@ -839,6 +839,102 @@ DEVI uint32_t r6_claim_reserved(r6_shared *sh, uint32_t lane, uint32_t wave, uin
 }
 #endif
 
+/* Bank-placed claims (round 4 A/B, R6_BANK_PLACE): the blocks of a round are read from the slot's period column, which
+ * sits in LDS bank slot % 32 (slot_lds: column 4 * (slot % 64), or 128 + 4 * (slot % 32), in rows of 256 bytes); two
+ * lanes of one 32-lane half whose slots share that residue conflict on every period read (3.3 % of the CU cycles, 1.3 %
+ * of the time: R6_PROBE_LANECOL).  Bit b of every bitmap word is a slot of residue b, so this claim takes, per residue,
+ * the first two queued slots of the class (over the words in order: at most 64, no two of a residue in one half) and
+ * places the first on lane b, the second on lane 32 + b; if that leaves room it fills the free lanes with further queued
+ * slots (those share a bank with a lane of their half).  Race and termination as in r6_claim: atomicAnd tells each word
+ * which chosen bits it got, every bit got is placed on a lane, unplaced lanes stay idle. */
+#ifndef R6_BANK_PLACE
+#define R6_BANK_PLACE 0
+#endif
+#ifndef R6_BANK_PLACE_FILL
+#define R6_BANK_PLACE_FILL 1      /* fill the lanes the first-two rule leaves free with further queued slots */
+#endif
+#if R6_BANK_PLACE
+DEVI uint32_t r6_wave_or(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
+    return v;
+}
+DEVI uint32_t r6_scan_add(uint32_t lane, uint32_t v) {    /* inclusive */
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+DEVI uint32_t r6_claim_placed(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t best) {
+    const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
+    /* inclusive scan of (residues seen at least once, at least twice) over the words */
+    uint32_t s1 = w, s2 = 0u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o1 = __shfl_up(s1, d, 64), o2 = __shfl_up(s2, d, 64);
+        if (lane >= (uint32_t)d) { s2 = s2 | o2 | (s1 & o1); s1 = s1 | o1; }
+    }
+    uint32_t e1 = __shfl_up(s1, 1, 64), e2 = __shfl_up(s2, 1, 64);
+    if (lane == 0) { e1 = 0u; e2 = 0u; }
+    const uint32_t r0 = w & ~e1, r1 = w & e1 & ~e2, ov = w & e2;
+    /* the first two of every residue (at most 64 in all), then further slots in word order while lanes are left */
+    /* one scan for both counts: the first-two slots (<= 64) in the low half, the others (<= R6_MAX_SLOTS) above */
+    const uint32_t pco = (uint32_t)__builtin_popcount(ov);
+    const uint32_t sc = r6_scan_add(lane, (uint32_t)__builtin_popcount(r0 | r1) | (pco << 16));
+    const uint32_t room = 64u - (__builtin_amdgcn_readlane(sc, 63) & 0xffffu), inc = sc >> 16;
+    uint32_t tov = 0u;
+    if (!R6_BANK_PLACE_FILL) {
+    } else if (inc <= room) {
+        tov = ov;
+    } else if (inc - pco < room) {
+        for (uint32_t k = room - (inc - pco), rest = ov; k; k--) {
+            tov |= rest & (0u - rest);
+            rest &= rest - 1u;
+        }
+    }
+    const uint32_t take = r0 | r1 | tov;
+    const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
+    const uint32_t g0 = got & r0, g1 = got & r1, gov = got & tov;
+    const uint32_t nov = (uint32_t)__builtin_popcount(gov);
+    const uint32_t sg = r6_scan_add(lane, (uint32_t)__builtin_popcount(got) | (nov << 16));
+    const uint32_t total = __builtin_amdgcn_readlane(sg, 63) & 0xffffu;
+    if (total == 0u) return 0;
+    sh->stage[wave][lane] = (uint16_t)0xffffu;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (uint32_t b = g0; b; b &= b - 1u) {
+        const uint32_t r = (uint32_t)__builtin_ctz(b);
+        sh->stage[wave][r] = (uint16_t)(lane * 32u + r);
+    }
+    for (uint32_t b = g1; b; b &= b - 1u) {
+        const uint32_t r = (uint32_t)__builtin_ctz(b);
+        sh->stage[wave][32u + r] = (uint16_t)(lane * 32u + r);
+    }
+    const uint32_t novt = __builtin_amdgcn_readlane(sg, 63) >> 16;           /* further slots got, wave total */
+    if (novt) {
+        const uint32_t u0 = r6_wave_or(g0), u1 = r6_wave_or(g1);
+        uint64_t fr = ~(((uint64_t)u1 << 32) | (uint64_t)u0);              /* lanes no residue owner took */
+        /* the k-th further slot (word order) on the k-th free lane: a uniform walk over the free lanes */
+        uint32_t j = (sg >> 16) - nov, rest = gov;
+        for (uint32_t k = 0; k < novt; k++) {
+            const uint32_t p = (uint32_t)__builtin_ctzll(fr);
+            fr &= fr - 1ull;
+            if (rest && j == k) {
+                sh->stage[wave][p] = (uint16_t)(lane * 32u + (uint32_t)__builtin_ctz(rest));
+                rest &= rest - 1u;
+                j++;
+            }
+        }
+    }
+    if (lane == 0) atomicSub(&sh->count[best], total);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
+    const uint32_t st = sh->stage[wave][lane];
+    *slot = st == 0xffffu ? R6_IDLE : st;
+    return total;
+}
+#endif
+
 /* Wave-uniform: claim up to 64 queued slots of the fullest class; returns how many (0: none queued) and
  * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
  * order up to 64 in total, clear exactly the bits they chose (atomicAnd returns what they got when another
@@ -863,6 +959,9 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
 #if R6_RESERVE
     /* range mode only: the list-mode instantiations spill 12 B/lane with it at the 168-VGPR limit */
     if (MODE == 0 && best < R6_CLASSES) return r6_claim_reserved(sh, lane, wave, slot, best);
+#endif
+#if R6_BANK_PLACE
+    if (MODE == 0 && best < R6_CLASSES) return r6_claim_placed(sh, lane, wave, slot, best);
 #endif
     const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
     const uint32_t pc = __builtin_popcount(w);
