@@ -62,6 +62,10 @@ def emulate(prog, keys, nk, sbase=0, text=None):
         vin["%%%d" % (21 + nkr)] = np.full(LANES, int(sel.group(1), 16), dtype=np.uint64)
         no = re.search(r"#define RC4_KSA_SELNOHIT (0x[0-9a-f]+)u", text)
         vin["%%%d" % (22 + nkr)] = np.full(LANES, int(no.group(1), 16), dtype=np.uint64)
+    idr = re.search(r"#define RC4_KSA_IDREGS (\d+)", text or "")
+    if idr:                                                # --idregs: identity rows as inputs after the key registers
+        for w in range(int(idr.group(1))):
+            vin["%%%d" % (21 + nkr + w)] = np.full(LANES, 0x03020100 + 0x04040404 * w, dtype=np.uint64)
     masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
     vcc = np.zeros(LANES, dtype=bool)
     M32 = np.uint64(0xffffffff)
@@ -229,7 +233,7 @@ def test_generated_ksa_equals_rc4(nk):
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
                                   "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add",
-                                  "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or"])
+                                  "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or", "--idregs 24"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
     group's S[j] stores and repairs it) compute the same key schedule."""
@@ -243,6 +247,20 @@ def test_schedule_variants_equal_rc4(flag):
         keys[0], keys[1], keys[2] = [0] * 16, [1] * 16, [2] * 16
         got = emulate(program(nk, text), keys, nk, text=text)
         assert all(got[l_] == ref_ksa(keys[l_], nk) for l_ in range(LANES)), (flag, nk)
+
+
+@pytest.mark.parametrize("flag", ["", "--idregs 24", "--and-or", "--jctr"])
+def test_m0_write_is_not_followed_by_an_lds_instruction(flag):
+    """gfx9 hazard: an instruction that reads M0 (ds_write_addtid_b32) needs one wait state after the s_mov that writes
+    M0; the emulator cannot see it (a variant that stored row 0 right behind the s_mov failed parity on the GPU)."""
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
+    for nk in (5, 16):
+        prog = program(nk, text)
+        for a, b in zip(prog, prog[1:]):
+            assert not (a.startswith("s_mov_b32 m0,") and b.startswith("ds_")), (flag, nk, a, b)
 
 
 def test_header_is_what_the_generator_writes():

@@ -71,7 +71,7 @@ def nkr_of(nk, jctr):
 
 
 def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False, ic4=False,
-        d16=False, split=False, b3addr=False):
+        d16=False, split=False, b3addr=False, idregs=0):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -89,7 +89,7 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
     if b128:
         identity_b128(e, IA, C16, D0)
     else:
-        identity(e, M, M0S, SB)
+        identity(e, M, M0S, SB, ["%%%d" % (21 + nkr + k) for k in range(idregs)])
     # jctr: byte 3 of j counts positions (the key registers carry +3 / -1 in byte 3 for even / odd steps), so after
     # step 0 of group q it is i1 and after step 1 it is i0: both compares read it from j itself.  Bytes 1-2 absorb the
     # carries and W's byte 1 (at most 128 x 0x101 per KSA < 2^16: nothing reaches byte 3).
@@ -285,11 +285,18 @@ def ksa_early_v1(nk):
     return out
 
 
-def identity(e, M, M0S, SB):
+def identity(e, M, M0S, SB, ids=()):
+    """ids (round 4 A/B, --idregs N): input VGPRs holding rows 0..N-1 of the identity (loop-invariant constants the
+    kernel keeps in registers), so only the rows after them need the add chain"""
     e("s_mov_b32 %s, m0" % M0S)
     e("s_mov_b32 m0, %s" % SB)
-    e("v_mov_b32 %s, 0x3020100" % M)
-    for w in range(64):
+    n = len(ids)
+    # the v_mov is also the wait state an M0 write needs before an LDS instruction that reads M0 (ds_write_addtid): a
+    # round-4 build that stored row 0 right behind the s_mov lost the identity's first row on the hardware
+    e("v_mov_b32 %s, 0x%x" % (M, (0x03020100 + 0x04040404 * n) & 0xffffffff))
+    for w in range(n):
+        e("ds_write_addtid_b32 %s offset:%d" % (ids[w], 256 * w))
+    for w in range(n, 64):
         e("ds_write_addtid_b32 %s offset:%d" % (M, 256 * w))
         if w < 63:
             e("v_add_u32 %s, 0x4040404, %s" % (M, M))
@@ -396,6 +403,10 @@ def main():
     # the address's low byte by v_bitop3 (full rate) instead of v_and_or (half rate): default since round 4 (R3/R4 625.7
     # -> 628.3 M, R2 12.38 -> 12.39 G, profiles/ab_r24_b3addr_r04n.txt); --and-or restores the old form
     b3addr = "--and-or" not in sys.argv
+    idregs = 0                          # round 4 A/B: --idregs N (identity rows 0..N-1 from N input VGPRs)
+    if "--idregs" in sys.argv:
+        idregs = int(sys.argv[sys.argv.index("--idregs") + 1])
+        assert not d16, "--idregs puts its inputs where --d16merge puts its selectors"
     # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
     # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
     jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
@@ -406,12 +417,16 @@ def main():
     print("   positions); 0 = the key byte in byte 0, anything above it.  RC4_KSA_NKR_5: registers of the 5-byte key */")
     print("#define RC4_KSA_KB_CTR %d" % (1 if jctr else 0))
     print("#define RC4_KSA_NKR_5 %d" % nkr_of(5, jctr))
+    if idregs:
+        print("#define RC4_KSA_IDREGS %d   /* identity rows 0..%d as input VGPRs after the keys (rc4_dev.h idc[]) */"
+              % (idregs, idregs - 1))
+        print("#define RC4_KSA_IDIN " + "".join(', "v"(idc[%d])' % k for k in range(idregs)))
     if d16:
         print("#define RC4_KSA_SELHIT 0x0c0c0400u   /* the block reads these two constants from the inputs after the keys */")
         print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
         lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
-                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr))
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr, idregs))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
