@@ -403,7 +403,9 @@ def main():
     # the address's low byte by v_bitop3 (full rate) instead of v_and_or (half rate): default since round 4 (R3/R4 625.7
     # -> 628.3 M, R2 12.38 -> 12.39 G, profiles/ab_r24_b3addr_r04n.txt); --and-or restores the old form
     b3addr = "--and-or" not in sys.argv
-    idregs = 0                          # round 4 A/B: --idregs N (identity rows 0..N-1 from N input VGPRs)
+    idregs = 0                          # round 4 A/B: --idregs N (identity rows 0..N-1 from N input VGPRs; measured +0.4 %
+    #                                     but failed the R4 list-mode verdict on the GPU, so the kernel-side hook -- an
+    #                                     idc[] array of the constants passed after the keys in rc4_dev.h -- was removed)
     if "--idregs" in sys.argv:
         idregs = int(sys.argv[sys.argv.index("--idregs") + 1])
         assert not d16, "--idregs puts its inputs where --d16merge puts its selectors"
