@@ -8,6 +8,27 @@
 #define ITERS 4096
 #define CHAINS 8
 
+/* round 4: does a wave64 VALU instruction cost less when a whole 32-lane half is inactive?  The add3 chain of OP 0 run
+ * by lanes < 32 only (90), by the even lanes only (91), by lanes < 16 (92) */
+template <int OP>
+__global__ void __launch_bounds__(256) kmask(unsigned *out, unsigned seed) {
+    const unsigned lane = threadIdx.x & 63u;
+    const bool on = OP == 90 ? lane < 32u : OP == 91 ? (lane & 1u) == 0u : lane < 16u;
+    if (!on) return;
+    unsigned x[CHAINS];
+    unsigned y = seed ^ threadIdx.x, z = seed * 3u + blockIdx.x;
+#pragma unroll
+    for (int c = 0; c < CHAINS; c++) x[c] = seed + c * 77u + threadIdx.x;
+    for (int i = 0; i < ITERS; i++) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; c++) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+    }
+    unsigned r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; c++) r ^= x[c];
+    if (r == 0x12345678u) out[0] = r;
+}
+
 template <int OP>
 __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
     unsigned x[CHAINS];
@@ -203,6 +224,30 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
 }
 
 template <int OP>
+double run_mask(const char *name, int blocks, double lanes_on) {
+    unsigned *d;
+    (void)hipMalloc(&d, 4);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(kmask<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a);
+    const int reps = 5;
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(kmask<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u + r);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    /* wave-instructions per second, whatever the active lanes: the cost of an instruction with a partial EXEC */
+    const double wave_instr = (double)reps * blocks * 4.0 * ITERS * CHAINS;
+    printf("%-28s %.3f ms  %.2f G wave-instr/s  (active-lane instr %.2f T/s)\n", name, ms / reps,
+           wave_instr / (ms / 1e3) / 1e9, wave_instr * lanes_on / (ms / 1e3) / 1e12);
+    (void)hipFree(d);
+    return ms;
+}
+
+template <int OP>
 double run(const char *name, int blocks, int per_iter) {
     unsigned *d;
     (void)hipMalloc(&d, 4);
@@ -256,6 +301,10 @@ int main(int argc, char **argv) {
         run<2>("v_alignbit_b32", blocks, 1);
         run<0>("v_add3_u32", blocks, 1);
         run<1>("v_bitop3_b32", blocks, 1);
+        run_mask<90>("add3, lanes 0-31 only", blocks, 32);
+        run_mask<91>("add3, even lanes only", blocks, 32);
+        run_mask<92>("add3, lanes 0-15 only", blocks, 16);
+        printf("(all 64 lanes: v_add3_u32 above, lane-instr/s / 64 = wave-instr/s)\n");
         printf("slot model for the mix: %.2f T lane-instr/s\n", 78.6432 * 8 / 14.4);
         return 0;
     }
