@@ -254,16 +254,36 @@ DEVI void aes128_expand_split(const r6_lds &S, const uint32_t key[4], uint32_t r
 #define R6_ASM_ROUND 1
 #endif
 #define R6_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
+/* R6_B1_BITOP3 (round 4, default): the four lookups per round that take byte 1 of a state word (term t = 2) form their
+ * address as (s & 0xff00) | (base >> 16 without its byte 1) -- ONE v_bitop3 (truth table 0xe2, full rate on gfx950
+ * with two VGPR sources) instead of a v_perm (half rate); base >> 16 is formed once per round inside the block (a
+ * long-lived register for it made the kernel spill 12 B/lane).  Measured: 3.743 -> 3.753 M cand/s (three alternating
+ * runs, profiles/ab_r6_b1_bitop3_r04t.txt).  The other three terms need a shift first (v_lshrrev + v_bitop3 for bytes
+ * 2 and 3, a half-rate v_lshlrev for byte 0): no fewer cycles than the v_perm. */
+#ifndef R6_B1_BITOP3
+#define R6_B1_BITOP3 1
+#endif
 DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
                        uint32_t k1, uint32_t k2, uint32_t k3) {
     uint32_t t[16];
 #define R6L(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
+#if R6_B1_BITOP3
+    /* base >> 16 in t[15]'s register: its own lookup (the last of the 16) comes after the four that read it */
+#define R6_B2PRE "v_lshrrev_b32 %19, 16, %20\n\t"
+#define R6L2(d, s) "v_bitop3_b32 %" #d ", %" #s ", %29, %19 bitop3:0xe2\n\tds_read_b32 %" #d ", %" #d "\n\t"
+#define R6_B2IN , "s"(0xff00u)
+#else
+#define R6_B2PRE
+#define R6L2(d, s) R6L(d, s, 27)
+#define R6_B2IN
+#endif
     asm volatile(
         /* column 0: s0 t0, s1 t1, s2 t2, s3 t3;  column 1: s1, s2, s3, s0;  column 2: s2, s3, s0, s1;  column 3 */
-        R6L(4, 0, 25) R6L(5, 1, 26) R6L(6, 2, 27) R6L(7, 3, 28)
-        R6L(8, 1, 25) R6L(9, 2, 26) R6L(10, 3, 27) R6L(11, 0, 28)
-        R6L(12, 2, 25) R6L(13, 3, 26) R6L(14, 0, 27) R6L(15, 1, 28)
-        R6L(16, 3, 25) R6L(17, 0, 26) R6L(18, 1, 27) R6L(19, 2, 28)
+        R6_B2PRE
+        R6L(4, 0, 25) R6L(5, 1, 26) R6L2(6, 2) R6L(7, 3, 28)
+        R6L(8, 1, 25) R6L(9, 2, 26) R6L2(10, 3) R6L(11, 0, 28)
+        R6L(12, 2, 25) R6L(13, 3, 26) R6L2(14, 0) R6L(15, 1, 28)
+        R6L(16, 3, 25) R6L(17, 0, 26) R6L2(18, 1) R6L(19, 2, 28)
         "s_waitcnt lgkmcnt(12)\n\t"
         "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
         "v_bitop3_b32 %0, %4, %7, %21 bitop3:0x96\n\t"
@@ -280,8 +300,11 @@ DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, u
           "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
           "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
         : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(R6_SEL(0)), "s"(R6_SEL(1)), "s"(R6_SEL(2)),
-          "s"(R6_SEL(3))
+          "s"(R6_SEL(3)) R6_B2IN
         : "memory");
+#undef R6_B2IN
+#undef R6_B2PRE
+#undef R6L2
 #undef R6L
 }
 
