@@ -453,15 +453,32 @@ __device__ constexpr int ODT_EPS[14] = {0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3, 0, 1
 #define ODT_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
 /* One inner round: 16 lookups issued column by column (column j: s_j, s_j-1, s_j-2, s_j-3 for lookups t = 0..3),
  * then each column's two v_bitop3 behind the wait covering its reads (as r6_round_asm). */
+/* ODT_B1_BITOP3 (round 4, as R6_B1_BITOP3 in dprf_kernels_r6.hip): the four byte-1 lookups of a round address their
+ * table by one full-rate v_bitop3 (s & 0xff00) | (base >> 16 without its byte 1) instead of a half-rate v_perm;
+ * base >> 16 is formed in t[15]'s register, whose own lookup comes last.  Measured neutral on ODF (1025.7 vs 1025.5 ms
+ * per 16 Mi-candidate step, profiles/ab_odt_b1_bitop3_r04v.txt: the check is ~2.4 % of a step), so off. */
+#ifndef ODT_B1_BITOP3
+#define ODT_B1_BITOP3 0
+#endif
 DEVI void odt_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
                         uint32_t k1, uint32_t k2, uint32_t k3) {
     uint32_t t[16];
 #define ODL(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
+#if ODT_B1_BITOP3
+#define ODT_B2PRE "v_lshrrev_b32 %19, 16, %20\n\t"
+#define ODL2(d, s) "v_bitop3_b32 %" #d ", %" #s ", %29, %19 bitop3:0xe2\n\tds_read_b32 %" #d ", %" #d "\n\t"
+#define ODT_B2IN , "s"(0xff00u)
+#else
+#define ODT_B2PRE
+#define ODL2(d, s) ODL(d, s, 27)
+#define ODT_B2IN
+#endif
     asm volatile(
-        ODL(4, 0, 25) ODL(5, 3, 26) ODL(6, 2, 27) ODL(7, 1, 28)
-        ODL(8, 1, 25) ODL(9, 0, 26) ODL(10, 3, 27) ODL(11, 2, 28)
-        ODL(12, 2, 25) ODL(13, 1, 26) ODL(14, 0, 27) ODL(15, 3, 28)
-        ODL(16, 3, 25) ODL(17, 2, 26) ODL(18, 1, 27) ODL(19, 0, 28)
+        ODT_B2PRE
+        ODL(4, 0, 25) ODL(5, 3, 26) ODL2(6, 2) ODL(7, 1, 28)
+        ODL(8, 1, 25) ODL(9, 0, 26) ODL2(10, 3) ODL(11, 2, 28)
+        ODL(12, 2, 25) ODL(13, 1, 26) ODL2(14, 0) ODL(15, 3, 28)
+        ODL(16, 3, 25) ODL(17, 2, 26) ODL2(18, 1) ODL(19, 0, 28)
         "s_waitcnt lgkmcnt(12)\n\t"
         "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
         "v_bitop3_b32 %0, %4, %7, %21 bitop3:0x96\n\t"
@@ -478,8 +495,11 @@ DEVI void odt_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, 
           "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
           "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
         : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(ODT_SEL(0)), "s"(ODT_SEL(1)), "s"(ODT_SEL(2)),
-          "s"(ODT_SEL(3))
+          "s"(ODT_SEL(3)) ODT_B2IN
         : "memory");
+#undef ODT_B2IN
+#undef ODT_B2PRE
+#undef ODL2
 #undef ODL
 }
 /* Si[byte K of v] from the row after the tables (address 0x10000 + x) */
