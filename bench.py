@@ -543,11 +543,14 @@ def main():
             out["device_balance"] = balance
         # every workload's figure in a few hundred bytes at the END of the line, so that a log tail shows all of
         # them (the 16 KB driver tail started inside the per-format CPU samples)
+        # kernel_ms is per launch; the launch size ("cand") lets it be compared per candidate with a profile whose
+        # rate-driven launches differ in size (R2-R4: launches also overlap on two streams)
         summ = {args.workload: {"value": out["value"], "valu_floor_frac": roof["frac"],
-                                "kernel_ms": m["avg_launch_ms"], "steps": args.steps}}
+                                "kernel_ms": m["avg_launch_ms"], "cand": int(m["per_launch"]), "steps": args.steps}}
         for name, v in side.items():
             summ[name] = {"value": v["value"], "valu_floor_frac": v["valu_floor_frac"],
-                          "kernel_ms": v["dominant_avg_ms"], "steps": v["steps"]}
+                          "kernel_ms": v["dominant_avg_ms"], "cand": int(v["candidates_per_launch"]),
+                          "steps": v["steps"]}
         if cluster and cluster.get("value") is not None:
             summ["cluster"] = {"value": cluster.get("value"), "clients": cluster.get("clients")}
         out["summary"] = {"build": build, "workloads": summ}
