@@ -836,6 +836,19 @@ DEVI void r24_ksa(uint8_t *S, uint32_t sbase, uint32_t lane, const uint32_t k[4]
     else rc4_ksa<NK>(S, lane << 2, k);
 }
 template <int R> struct r24_batches { static constexpr uint32_t v = R == 2 ? R2_BATCHES : R34_BATCHES; };
+#ifdef DPRF_DEBUG_R24
+/* Debug builds only (round 5, tools/r24_dump.py): workgroup 0, batch 0 of k_pdf_r24 R3/R4 records its keys, the data
+ * words after every pass of both sweeps and lane 0's S-box after each pass of sweep 0, so a wrong verdict on the
+ * hardware can be traced to the first pass / KSA that differs from a CPU RC4 chain.  Layout (words):
+ * [0, 256) h[4] per lane; [256, 10496) d[4] per (sweep, pass, lane); [10496, 11776) S-box of lane 0 per sweep-0 pass
+ * (64 words each); [11776] the number of sweeps run. */
+#define R24_DBG_WORDS 11784
+__device__ uint32_t g_r24_dbg[R24_DBG_WORDS];
+extern "C" int dprf_debug_r24_read(uint32_t *out, size_t nwords) {
+    if (nwords > R24_DBG_WORDS) nwords = R24_DBG_WORDS;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_r24_dbg), nwords * 4, 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int MODE, int R, int NK>
 __global__ void __launch_bounds__(128, 5)   /* 18 waves per CU (9 workgroups): <= 102 VGPRs */
 k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
@@ -955,8 +968,25 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
                     uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
                     rc4_ksa<NK>(Sw, lane << 2, kx);
                 }
+#ifdef DPRF_DEBUG_R24
+                if (blockIdx.x == 0 && b == 0 && !full) {
+                    if (x == 0) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) g_r24_dbg[4 * lane + q] = h[q];
+                    }
+                    if (lane == 0)
+                        for (int w = 0; w < 64; w++) g_r24_dbg[10496 + 64 * x + w] = *(const uint32_t *)(Sw + 256 * w);
+                }
+#endif
                 if (full) rc4_prga<16>(Sw, lane << 2, d);
                 else rc4_prga<2>(Sw, lane << 2, d);
+#ifdef DPRF_DEBUG_R24
+                if (blockIdx.x == 0 && b == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) g_r24_dbg[256 + ((full * 20u + x) * 64u + lane) * 4u + q] = d[q];
+                    if (lane == 0) g_r24_dbg[11776] = full + 1u;
+                }
+#endif
             }
             if (full) {
                 ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];

@@ -157,6 +157,12 @@ DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc
 #ifdef RC4_KSA_SELHIT
     const uint32_t selhit = RC4_KSA_SELHIT, selno = RC4_KSA_SELNOHIT;
 #define RC4_KSA_XIN , "v"(selhit), "v"(selno)
+#elif defined(RC4_KSA_IDREGS)
+    /* A/B headers with the first identity rows as inputs (gen_rc4_ksa_asm.py --idregs): loop-invariant constants */
+    uint32_t idc[RC4_KSA_IDREGS];
+#pragma unroll
+    for (int w = 0; w < RC4_KSA_IDREGS; w++) idc[w] = 0x03020100u + 0x04040404u * (uint32_t)w;
+#define RC4_KSA_XIN RC4_KSA_IDIN
 #else
 #define RC4_KSA_XIN
 #endif

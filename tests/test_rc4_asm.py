@@ -115,6 +115,27 @@ def emulate(prog, keys, nk, sbase=0, text=None):
                 lds[addr:addr + 4] = np.frombuffer(int(v(d)[l_]).to_bytes(4, "little"), dtype=np.uint8)
         elif op == "v_add_u32":
             regs[a[0]] = (v(a[1]) + v(a[2])) & M32
+        elif op == "v_lshlrev_b32":                          # dst = src1 << (src0 & 31)
+            regs[a[0]] = (v(a[2]) << (v(a[1]) & np.uint64(31))) & M32
+        elif op == "v_lshrrev_b32":
+            regs[a[0]] = (v(a[2]) & M32) >> (v(a[1]) & np.uint64(31))
+        elif op == "v_bfm_b32":                              # ((1 << src0) - 1) << src1, 5-bit fields
+            w_ = (np.uint64(1) << (v(a[1]) & np.uint64(31))) - np.uint64(1)
+            regs[a[0]] = (w_ << (v(a[2]) & np.uint64(31))) & M32
+        elif op == "v_lshlrev_b32_sdwa":
+            assert "src1_sel:BYTE_0" in ln and "dst_sel:DWORD" in ln and "src0_sel:DWORD" in ln
+            regs[a[0]] = ((v(a[2].split()[0]) & np.uint64(0xff)) << (v(a[1]) & np.uint64(31))) & M32
+        elif op == "ds_mskor_rtn_b32":                       # MEM = (MEM & ~DATA0) | DATA1, old dword returned
+            ad = v(a[1]).astype(np.int64)
+            assert bool(np.all(ad % 4 == 0)), "mskor address not dword-aligned"
+            old = np.zeros(LANES, dtype=np.uint64)
+            for b in range(4):
+                old |= lds[ad + b].astype(np.uint64) << np.uint64(8 * b)
+            new = (old & ~v(a[2]) & M32) | v(a[3])
+            assert bool(np.all(new <= M32))
+            for b in range(4):
+                lds[ad + b] = ((new >> np.uint64(8 * b)) & np.uint64(0xff)).astype(np.uint8)
+            regs[a[0]] = old
         elif op == "v_add3_u32":
             regs[a[0]] = (v(a[1]) + v(a[2]) + v(a[3])) & M32
         elif op == "v_and_or_b32":
@@ -214,6 +235,107 @@ def emulate(prog, keys, nk, sbase=0, text=None):
     return out
 
 
+def lds_hazards(prog):
+    """What emulate() cannot see: LDS is asynchronous.  A ds_read's result lands in its VGPR some time after issue --
+    the block may only rely on it after an s_waitcnt lgkmcnt(N) that leaves at most N younger LDS operations in flight
+    (LDS completes in order, stores count too).  Every instruction reads its VGPR sources AT ISSUE, including
+      - a destination the instruction only partly writes (SDWA dst_unused:UNUSED_PRESERVE), and
+      - the destination of a d16 load (ds_read_u8_d16 / _d16_hi keep the other half: LLVM models the old value as a
+        tied source operand, and the hardware merges with the value the VGPR holds when the load ISSUES).
+    And one wait-state rule of gfx9 the hardware does not interlock: an instruction that reads M0 (ds_write_addtid_b32
+    forms its address from M0) needs one wait state after the SALU write of M0 -- without it the store uses the OLD M0.
+    Returns [(line index, hazard)] for every read of, or VALU write to, a VGPR whose load has not been waited for,
+    and for every M0 reader right behind an M0 write."""
+    pending = []             # LDS operations in flight, oldest first: the destination VGPR of a load, None for a store
+    out = []
+
+    def vregs(toks):
+        return [t for t in toks if t.startswith("%") or re.match(r"v\d+$", t)]
+
+    for k, ln in enumerate(prog):
+        op, _, rest = ln.partition(" ")
+        a = [t.strip().split()[0] for t in rest.split(",") if t.strip()]
+        if op == "ds_write_addtid_b32" and k and prog[k - 1].startswith("s_mov_b32 m0,"):
+            out.append((k, "M0 read with no wait state after the M0 write: %s" % ln))
+        if op == "s_waitcnt":
+            n = int(re.search(r"lgkmcnt\((\d+)\)", ln).group(1))
+            while len(pending) > n:
+                pending.pop(0)
+            continue
+        if op.startswith("s_"):
+            continue
+        if op.startswith("ds_read") or "_rtn_" in op:
+            dst, srcs = a[0], vregs(a[1:])
+            if "_d16" in op:
+                srcs = srcs + [dst]
+        elif op.startswith("ds_write"):
+            dst, srcs = None, vregs(a)
+        elif op.startswith("v_cmp"):
+            dst, srcs = None, vregs(a[1:])
+        else:
+            dst, srcs = a[0], vregs(a[1:])
+            if "UNUSED_PRESERVE" in ln:
+                srcs = srcs + [dst]
+        for r in srcs:
+            if r in pending:
+                why = ("d16 load reads its destination at issue" if (op.startswith("ds_read") and r == dst)
+                       else "read before its LDS load was waited for")
+                out.append((k, "%s: %s (%s)" % (why, ln, r)))
+        if dst is not None and not op.startswith("ds_") and dst in pending:
+            out.append((k, "VALU write of a VGPR with an LDS load in flight: %s" % ln))
+        if op.startswith("ds_"):
+            pending.append(dst)
+    return out
+
+
+@pytest.mark.parametrize("flag", ["", "--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
+                                  "--jctr", "--early-v1", "--ic4", "--split-add", "--split-add --ic4", "--and-or",
+                                  "--idregs 24", "--mskor"])
+def test_schedule_waits_cover_every_lds_result(flag):
+    """Every schedule the GPU ran green reads an LDS result only after an lgkmcnt wait that covers it."""
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
+    for nk in (5, 16):
+        assert lds_hazards(program(nk, text)) == [], (flag, nk, lds_hazards(program(nk, text))[:3])
+
+
+@pytest.mark.parametrize("flag", ["--d16merge", "--ic4 --d16merge", "--split-add --ic4 --d16merge"])
+def test_d16_merge_schedule_is_rejected(flag):
+    """Round 4's --d16merge variant computed wrong S-boxes on the MI355X (profiles/ab_r24_d16merge_r04b.log) although
+    emulate() passes it: x1's ds_read_u8_d16_hi into the register x0's ds_read_u8_d16 is still filling reads that
+    register at issue, so the low half it keeps is the stale one.  The hazard model names it."""
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
+    for nk in (5, 16):
+        hz = lds_hazards(program(nk, text))
+        assert hz and all("d16 load reads its destination at issue" in h for _, h in hz), (flag, nk, hz[:3])
+
+
+def test_idregs_without_the_m0_wait_state_is_rejected():
+    """The first round-4 --idregs build (identity rows 0..23 from input VGPRs) stored row 0 right behind the M0 write
+    and failed the R4 verdict table on the MI355X (gpurun_out/id24_tests.log, 23:39); emulate() passes it.  Round 5
+    re-ran that schedule in tools/rc4_ksa_probe.hip on the MI355X (profiles/rc4_ksa_probe_r05.txt): row 0 wrong.  With
+    the wait state (the generator's default since dc0a9da) the probe, the verdict tables and the per-pass trace of
+    tools/r24_dump.py are green (profiles/rc4_ksa_probe_r05.txt)."""
+    import subprocess
+    import sys
+    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
+    text = subprocess.run([sys.executable, gen, "--idregs", "24", "--no-m0-wait"], capture_output=True, text=True,
+                          check=True).stdout
+    for nk in (5, 16):
+        prog = program(nk, text)
+        hz = lds_hazards(prog)
+        assert len(hz) == 1 and "M0 read with no wait state" in hz[0][1], (nk, hz)
+        rng = random.Random(7)
+        keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
+        got = emulate(prog, keys, nk, text=text)        # the dataflow alone is right: only the hazard model sees it
+        assert all(got[l_] == ref_ksa(keys[l_], nk) for l_ in range(LANES))
+
+
 @pytest.mark.parametrize("nk", [5, 16])
 def test_generated_ksa_equals_rc4(nk):
     if not os.path.exists(HDR):
@@ -232,7 +354,7 @@ def test_generated_ksa_equals_rc4(nk):
 
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add",
+                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add", "--mskor",
                                   "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or", "--idregs 24"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this

@@ -51,6 +51,10 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     d16 loads into one register, merged by one v_perm)
        tools/gen_rc4_ksa_asm.py --and-or > <variant header>        (the S[j] address's low byte by v_and_or_b32, half
                                                                     rate, as before round 4; default: v_bitop3_b32)
+       tools/gen_rc4_ksa_asm.py --mskor > <variant header>          (round 5 A/B: S[j] read + store as one
+                                                                    ds_mskor_rtn_b32: 4 LDS ops per group, 18 VALU)
+       tools/gen_rc4_ksa_asm.py --idregs 24 [--no-m0-wait] > <hdr>  (round 4 A/B: identity rows 0-23 from input VGPRs;
+                                                                    --no-m0-wait: round 4's first, wrong, schedule)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
                                                                     64-bit adds: 612 -> 595 M, the b128 stores cost
                                                                     more LDS time than the instructions they save)
@@ -71,7 +75,7 @@ def nkr_of(nk, jctr):
 
 
 def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b128=False, jctr=False, ic4=False,
-        d16=False, split=False, b3addr=False, idregs=0):
+        d16=False, split=False, b3addr=False, idregs=0, m0_wait=True):
     # operands: %0 j, %1 W, %2 x0, %3 x1, %4 v1, %5 a0, %6 a1, %7 m, %8 stmp (SGPR), %9 m0save (SGPR), %10 Wn / IC,
     #           %11-%15 SGPR pairs (prefetch repairs: j0 == p2, j0 == p3, j1 == p2, j1 == p3; hit0),
     #           %16 lanebase, %17 sbase (SGPR, the area's LDS address for ds_write_addtid), %18 identity address
@@ -89,7 +93,7 @@ def ksa(nk, early_read=False, late_merge=False, prefetch=False, vconst=False, b1
     if b128:
         identity_b128(e, IA, C16, D0)
     else:
-        identity(e, M, M0S, SB, ["%%%d" % (21 + nkr + k) for k in range(idregs)])
+        identity(e, M, M0S, SB, ["%%%d" % (21 + nkr + k) for k in range(idregs)], m0_wait)
     # jctr: byte 3 of j counts positions (the key registers carry +3 / -1 in byte 3 for even / odd steps), so after
     # step 0 of group q it is i1 and after step 1 it is i0: both compares read it from j itself.  Bytes 1-2 absorb the
     # carries and W's byte 1 (at most 128 x 0x101 per KSA < 2^16: nothing reaches byte 3).
@@ -285,17 +289,93 @@ def ksa_early_v1(nk):
     return out
 
 
-def identity(e, M, M0S, SB, ids=()):
+def ksa_mskor(nk):
+    """Round 5 A/B (VERDICT r4 "next" #2): each S[j] read + S[j] byte store fused into ONE ds_mskor_rtn_b32 on the
+    dword holding S[j] -- MEM = (MEM & ~mask) | data, the old dword returned -- with mask = 0xff << 8 (j & 3) (v_bfm)
+    and data = S[i] << 8 (j & 3); S[j] is the returned dword >> 8 (j & 3).  4 LDS operations per group instead of 6,
+    for 6 more VALU (12 -> 18 per group): the S[j] address loses its (j & 3) byte-0 term (the address registers keep
+    lanebase in bytes 0, 2, 3 across steps, only byte 1 is re-inserted), the shift amount sh = j << 3 (only its low
+    5 bits are read), the mask, the data shift and one extract per step.  vconst compare constants as the default."""
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, IA, C16, D0 = (
+        "%%%d" % k for k in range(21))
+    # scratch VGPRs of this variant: the prefetch variant's SGPR-pair outputs are not used here, so the shift amounts,
+    # masks and data words take the clobbered v60-v63 (sh0 / sh1 live until the extracts) and M / IA-free outputs
+    SH0, SH1, MK, DT = "v60", "v61", "v62", "v63"
+    KB = ["%%%d" % (21 + k) for k in range(nk)]
+    out = []
+    e = out.append
+    identity(e, M, M0S, SB)
+    e("v_mov_b32 %s, 0" % J)
+    e("v_mov_b32 %s, 0x100" % W)
+    e("v_mov_b32 %s, %s" % (A0, LB))      # byte 1 is replaced per step; bytes 0, 2, 3 stay lanebase's
+    e("v_mov_b32 %s, %s" % (A1, LB))
+    IC = WN
+    FIRST_IC = 32
+    e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
+
+    def cmp(i, sel):
+        if q < FIRST_IC:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i))
+        else:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:%s" % (J, IC, sel))
+
+    for q in range(128):
+        i0, i1 = 2 * q, 2 * q + 1
+        if q > 0:
+            e("s_waitcnt lgkmcnt(1)")
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W, KB[i0 % nk]))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A0, J))
+        e("v_lshlrev_b32 %s, 3, %s" % (SH0, J))
+        cmp(i1, "BYTE_1")
+        e("v_bfm_b32 %s, 8, %s" % (MK, SH0))
+        e("v_lshlrev_b32_sdwa %s, %s, %s dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+          % (DT, SH0, W))
+        e("ds_mskor_rtn_b32 %s, %s, %s, %s" % (X0, A0, MK, DT))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_0"
+          % (V1, W, W))
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A1, J))
+        e("v_lshlrev_b32 %s, 3, %s" % (SH1, J))
+        cmp(i0, "BYTE_0")
+        e("v_bfm_b32 %s, 8, %s" % (MK, SH1))
+        e("v_lshlrev_b32 %s, %s, %s" % (DT, SH1, V1))
+        e("ds_mskor_rtn_b32 %s, %s, %s, %s" % (X1, A1, MK, DT))
+        if FIRST_IC <= q < 127:
+            e("v_add_u32 %s, 0x202, %s" % (IC, IC))
+        if q < 127:
+            e("ds_read_u16 %s, %s offset:%d" % (W, LB, pos(i0 + 2)))
+            e("s_waitcnt lgkmcnt(1)")
+        else:
+            e("s_waitcnt lgkmcnt(0)")
+        e("v_lshrrev_b32 %s, %s, %s" % (X0, SH0, X0))
+        e("v_lshrrev_b32 %s, %s, %s" % (X1, SH1, X1))
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))
+        e("v_cndmask_b32_sdwa %s, %s, %s, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+          % (M, X1, X0))
+        e("ds_write_b16 %s, %s offset:%d" % (LB, M, pos(2 * q)))
+    e("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def identity(e, M, M0S, SB, ids=(), m0_wait=True):
     """ids (round 4 A/B, --idregs N): input VGPRs holding rows 0..N-1 of the identity (loop-invariant constants the
     kernel keeps in registers), so only the rows after them need the add chain"""
     e("s_mov_b32 %s, m0" % M0S)
     e("s_mov_b32 m0, %s" % SB)
     n = len(ids)
-    # the v_mov is also the wait state an M0 write needs before an LDS instruction that reads M0 (ds_write_addtid): a
-    # round-4 build that stored row 0 right behind the s_mov lost the identity's first row on the hardware
-    e("v_mov_b32 %s, 0x%x" % (M, (0x03020100 + 0x04040404 * n) & 0xffffffff))
+    # the v_mov is also the wait state an M0 write needs before an LDS instruction that reads M0 (ds_write_addtid): the
+    # first round-4 --idregs build stored row 0 right behind the s_mov and lost it on the hardware (the write used the
+    # old M0).  --no-m0-wait regenerates that schedule (round 5: tools/rc4_ksa_probe.hip shows rows 0 wrong on the
+    # MI355X; tests/test_rc4_asm.py's hazard model rejects it)
+    mov = "v_mov_b32 %s, 0x%x" % (M, (0x03020100 + 0x04040404 * n) & 0xffffffff)
+    if m0_wait or not n:
+        e(mov)
     for w in range(n):
         e("ds_write_addtid_b32 %s offset:%d" % (ids[w], 256 * w))
+    if not (m0_wait or not n):
+        e(mov)
     for w in range(n, 64):
         e("ds_write_addtid_b32 %s offset:%d" % (M, 256 * w))
         if w < 63:
@@ -403,12 +483,16 @@ def main():
     # the address's low byte by v_bitop3 (full rate) instead of v_and_or (half rate): default since round 4 (R3/R4 625.7
     # -> 628.3 M, R2 12.38 -> 12.39 G, profiles/ab_r24_b3addr_r04n.txt); --and-or restores the old form
     b3addr = "--and-or" not in sys.argv
-    idregs = 0                          # round 4 A/B: --idregs N (identity rows 0..N-1 from N input VGPRs; measured +0.4 %
-    #                                     but failed the R4 list-mode verdict on the GPU, so the kernel-side hook -- an
-    #                                     idc[] array of the constants passed after the keys in rc4_dev.h -- was removed)
+    # identity rows 0..N-1 from N loop-invariant input VGPRs (rc4_dev.h idc[]): 23 fewer instructions per KSA.  Round 4
+    # measured +0.4 % and saw the R4 verdict table fail on the MI355X; round 5 traced that failure to the schedule
+    # without the M0 wait state (--no-m0-wait, tools/rc4_ksa_probe.hip: wrong S-boxes) and re-measured the fixed one:
+    # green on the R2-R4 parity tests, R3/R4 625.5 vs 623.1 M, R2 12.34 vs 12.29 G (profiles/ab_r24_r05b.txt), so 24 is
+    # the default since round 5 (--idregs 0: the add chain for every row, as before)
+    own = any(f in sys.argv for f in ("--d16merge", "--b128-identity", "--prefetch", "--early-v1", "--mskor"))
+    idregs = 0 if own else 24           # the variants with an identity / operand layout of their own take none
     if "--idregs" in sys.argv:
         idregs = int(sys.argv[sys.argv.index("--idregs") + 1])
-        assert not d16, "--idregs puts its inputs where --d16merge puts its selectors"
+        assert not (d16 and idregs), "--idregs puts its inputs where --d16merge puts its selectors"
     # --jctr: the j-counter schedule (measured round 3: 19 instructions per group but 1.3 % slower than the vconst
     # schedule on R3/R4 and R2 -- the compare reading j twice costs more than the v_add it saves); default: vconst
     jctr = "--jctr" in sys.argv and not (early or late or pre or b128 or "--salu-consts" in sys.argv)
@@ -427,8 +511,9 @@ def main():
         print("#define RC4_KSA_SELHIT 0x0c0c0400u   /* the block reads these two constants from the inputs after the keys */")
         print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
-        lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else
-                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr, idregs))
+        lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else ksa_mskor(nk) if "--mskor" in sys.argv else
+                 ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr, idregs,
+                     "--no-m0-wait" not in sys.argv))
         print("#define RC4_KSA_ASM_%d \\" % nk)
         for ln in lines:
             print('    "%s\\n\\t" \\' % ln)
