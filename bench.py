@@ -297,6 +297,18 @@ def measured_bound(counters, wkey):
     return work.BOUND.get(wkey, "valu"), "model"
 
 
+def latency_roof(wkey, per_gpu_rate):
+    """R2-R4: the chain-latency bound (dprf_amd/work.py lds_latency_bound: 9 chains per CU at the unloaded chain
+    latency tools/rc4_ksa_probe.hip measured) and the fraction of it this run reached, from its per-GPU wall rate"""
+    from dprf_amd import work
+    b = work.lds_latency_bound(wkey)
+    if b is None:
+        return None
+    return {"bound_cand_per_s": b, "frac": per_gpu_rate / b, "chains_per_cu": work.RC4_CHAINS_PER_CU,
+            "pass_ns_unloaded": work.RC4_PASS_NS_UNLOADED[wkey], "passes_per_candidate": work.RC4_PASSES[wkey],
+            "source": work.RC4_LATENCY_SOURCE}
+
+
 def compact_rocprof(rec):
     return None if not rec else {k: rec[k] for k in ROCPROF_KEYS if rec.get(k) is not None}
 
@@ -337,8 +349,10 @@ def summarize(stats, wkey, world, dt):
     per_launch = cands / max(1, launches)
     floor = work.per_candidate(wkey, part="main")
     achieved = per_launch * floor / (avg_launch_ms / 1e3)
+    spec = work.per_candidate(wkey, "spec", part="main")
     return {"cands": cands, "launches": launches, "kern_ms": kern_ms, "avg_launch_ms": avg_launch_ms,
             "per_launch": per_launch, "floor": floor, "achieved": achieved,
+            "spec": spec, "achieved_spec": per_launch * spec / (avg_launch_ms / 1e3),
             # host time of the library calls not covered by device time (launch gaps, polling, hit merge)
             "call_overhead": 1.0 - kern_ms / max(1e-9, wall_ms * devs),
             "value": cands * world / dt}
@@ -425,10 +439,9 @@ def main():
                     continue
                 sn, scs, spl, _, _, _ = WORKLOADS[name]
                 sf = quiet_fields(brute_force, S[sn]["stream"])
-                # configs[0] IS "brute_force.py on CPU": Office gets the full set (1 worker, 4-process model)
-                side_cpu[name] = (cpu_baselines(sf, scs, spl, seconds=min(1.0, args.cpu_seconds))
-                                  if name == "office" else
-                                  cpu_baseline(sf, scs, spl, seconds=min(1.0, args.cpu_seconds)))
+                # every format gets brute_force.py's own structure (4 processes, one Popen of the reference verifier
+                # per candidate), 1 worker and all cores of the job's share (round 5)
+                side_cpu[name] = cpu_baselines(sf, scs, spl, seconds=min(1.0, args.cpu_seconds))
 
     ctx = _lib.Context(fields, devices=devices)
     B = args.batch or B
@@ -464,7 +477,15 @@ def main():
                           "valu_floor_frac": max(sm["per_launch"] * work.per_candidate(skey)
                                                  / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak,
                                                  sm["value"] / world / max(1, len(devices)) * work.per_candidate(skey) / peak),
+                          # SURVEY 8(d)'s spec-level ops per candidate over the same peak, same time base
+                          "spec_frac": max(sm["per_launch"] * work.per_candidate(skey, "spec")
+                                           / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak,
+                                           sm["value"] / world / max(1, len(devices)) * work.per_candidate(skey, "spec") / peak),
                           "call_overhead": sm["call_overhead"]}
+            lat = latency_roof(skey, sm["value"] / world / max(1, len(devices)))
+            if lat:
+                side[name]["bound"] = "lds-latency"
+                side[name]["lds_latency"] = lat
             if skey in work.LDS_CYCLES:             # RC4 formats: the modelled LDS-array share (~ rocprof LdsUtil)
                 side[name]["lds_cycle_frac"] = work.lds_frac(
                     skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
@@ -497,7 +518,10 @@ def main():
         bound, bound_src = measured_bound(counters, wkey)
         roof = {"bound": bound, "bound_source": bound_src, "achieved": m["achieved"] / 1e12, "peak": peak / 1e12,
                 "unit": "T VALU lane-slots/s (gfx950 issue-slot floor of the algorithm)",
-                "frac": m["achieved"] / peak, "traffic": traffic,
+                "frac": m["achieved"] / peak, "valu_floor_frac": m["achieved"] / peak,
+                # the same kernel time against SURVEY 8(d)'s spec-level op count (2-input ops, 3-input = 2)
+                "spec_frac": m["achieved_spec"] / peak, "spec_achieved": m["achieved_spec"] / 1e12,
+                "traffic": traffic,
                 "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),
                 "kernel_avg_ms": m["avg_launch_ms"], "candidates_per_launch": m["per_launch"],
                 "floor_instr_per_candidate": m["floor"],
@@ -506,6 +530,11 @@ def main():
                 "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
                 "lds_cycle_frac": work.lds_frac(wkey, m["per_launch"] / (m["avg_launch_ms"] / 1e3)),
                 "call_overhead": m["call_overhead"]}
+        lat = latency_roof(wkey, m["value"] / world / max(1, len(devices)))
+        if lat:             # R2-R4: quoted against the chain-latency bound the design can approach (work.py)
+            roof["lds_latency"] = lat
+            roof.update(bound="lds-latency", bound_source="model: 9 chains/CU at the unloaded chain latency "
+                        "(tools/rc4_ksa_probe.hip)", frac=lat["frac"])
         if traffic_rec:
             roof["traffic_source"] = {k: traffic_rec.get(k) for k in ("source", "build", "stale", "fetch_bytes",
                                                                       "write_bytes", "bytes_per_candidate")}
@@ -545,12 +574,25 @@ def main():
         # them (the 16 KB driver tail started inside the per-format CPU samples)
         # kernel_ms is per launch; the launch size ("cand") lets it be compared per candidate with a profile whose
         # rate-driven launches differ in size (R2-R4: launches also overlap on two streams)
-        summ = {args.workload: {"value": out["value"], "valu_floor_frac": roof["frac"],
-                                "kernel_ms": m["avg_launch_ms"], "cand": int(m["per_launch"]), "steps": args.steps}}
+        def cpu_short(c):
+            """the CPU figures of a leg, cand/s: all cores of the share / 1 worker / brute_force.py's 4 processes"""
+            if not c:
+                return None
+            g = lambda k: round(c[k]["value"], 1) if c.get(k) else None
+            return {"all": round(c["value"], 1), "cores": c.get("cores"), "one": g("one_worker"),
+                    "pm4": g("process_model_4")}
+
+        summ = {args.workload: {"value": out["value"], "valu_floor_frac": roof["valu_floor_frac"], "spec_frac": roof["spec_frac"],
+                                "kernel_ms": m["avg_launch_ms"], "cand": int(m["per_launch"]), "steps": args.steps,
+                                "cpu": cpu_short(cpu)}}
+        if roof.get("lds_latency"):
+            summ[args.workload]["lds_latency_frac"] = roof["lds_latency"]["frac"]
         for name, v in side.items():
-            summ[name] = {"value": v["value"], "valu_floor_frac": v["valu_floor_frac"],
+            summ[name] = {"value": v["value"], "valu_floor_frac": v["valu_floor_frac"], "spec_frac": v["spec_frac"],
                           "kernel_ms": v["dominant_avg_ms"], "cand": int(v["candidates_per_launch"]),
-                          "steps": v["steps"]}
+                          "steps": v["steps"], "cpu": cpu_short(side_cpu.get(name))}
+            if v.get("lds_latency"):
+                summ[name]["lds_latency_frac"] = v["lds_latency"]["frac"]
         if cluster and cluster.get("value") is not None:
             summ["cluster"] = {"value": cluster.get("value"), "clients": cluster.get("clients")}
         out["summary"] = {"build": build, "workloads": summ}

@@ -43,6 +43,9 @@ ROUND_SECONDS = 5.0              # range mode: wall time of one library call (ch
 FIRST_ROUND = 1 << 22           # least candidates of the first round, before a rate is known
 ROUND_CHUNKS = 4                 # a round lasts at least this many of the library's largest chunks (0: fixed
                                  # FIRST_ROUND / ROUND_SECONDS only)
+ROUND_MAX_SECONDS = 12.0         # ... but never longer (R6's 2^25-candidate chunks, ~9 s each, would make
+                                 # multi-GPU rounds ~36 s -- the checkpoint / Ctrl-C granularity; the guided split of
+                                 # dprf_plan_chunk sizes the chunks of a shorter round down by itself)
 _HUGE = 1 << 62
 
 
@@ -140,7 +143,7 @@ def round_seconds(kernel, rate, ndev):
     if per_dev_ms <= 0 or not ROUND_CHUNKS or kernel is None or ndev <= 1:
         return ROUND_SECONDS
     big = _lib.plan_chunk(kernel, per_dev_ms, _HUGE, _HUGE, 1)
-    return max(ROUND_SECONDS, ROUND_CHUNKS * big / per_dev_ms / 1e3)
+    return min(ROUND_MAX_SECONDS, max(ROUND_SECONDS, ROUND_CHUNKS * big / per_dev_ms / 1e3))
 
 
 def next_round(rate, remaining, seconds=ROUND_SECONDS, first=FIRST_ROUND):

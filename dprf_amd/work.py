@@ -4,7 +4,16 @@ Peak.  gfx950 issues one wave64 VALU instruction per SIMD every 2 cycles for FUL
 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.64e12 lane-slots/s.  Measured on MI355X
 (profiles/valu_issue_rates_r01.txt, tools/valu_peak.hip): v_add/v_sub/v_xor/v_and/v_or/v_not/v_lshrrev_b32
 reach 96-98% of that; v_lshlrev_b32, v_alignbit (rotate), v_alignbyte, v_perm, v_bfe, v_add3, v_and_or,
-v_lshl_or, v_sad_u8, v_mul_u32_u24 issue at half rate (2 slots); v_bitop3 at 0.59 (1.7 slots).
+v_lshl_or, v_sad_u8, v_mul_u32_u24 issue at half rate (2 slots).  v_bitop3_b32 issues at FULL rate (1 slot) whenever
+its three sources are not all in one VGPR bank (register index mod 4): tools/valu_peak.hip mix "bitop3|xor indep"
+76.1 T = 96.8 % (profiles/valu_mix_r04.txt), tools/vgpr_bank.hip 95-98 % with sources in banks 0,1,2 or 0,1,0 and
+49 % only with 0,0,0 (profiles/vgpr_bank_r04.txt); the compiled KDF loops have no three-same-bank bitop3.  Until
+round 5 this table charged it 1.7 slots -- the single-op probe's own register allocation (0,0,0), not the kernels'.
+
+What the additive table does not model: a stream that MIXES half- and full-rate instructions issues slower than the
+sum of their slots (profiles/valu_mix_r04.txt: 50/50 independent 3.74 cycles per wave-instruction against 3.0
+additive; the ODF KDF loop's own 21-instruction pattern 3.75 against 3.24), so a kernel at the issue limit of its
+own mix shows floor fractions ~0.85-0.9, not 1.0.
 
 Floor.  The per-candidate work is the fewest issue slots the ALGORITHM needs on gfx950 with that cost
 table, derived per primitive from its dataflow (sha1_floor() below does it exactly from which message
@@ -18,7 +27,7 @@ PEAK_SLOTS_PER_S = 256 * 4 * 32 * 2.4e9   # 78.64e12 full-rate VALU lane-slots/s
 PEAK_LANE_INSTR_PER_S = PEAK_SLOTS_PER_S   # backwards-compatible name
 
 # measured issue cost in full-rate slots
-COST = {"add": 1.0, "xor": 1.0, "and": 1.0, "or": 1.0, "shr": 1.0, "shl": 2.0, "rot": 2.0, "bitop3": 1.7,
+COST = {"add": 1.0, "xor": 1.0, "and": 1.0, "or": 1.0, "shr": 1.0, "shl": 2.0, "rot": 2.0, "bitop3": 1.0,
         "add3": 2.0, "perm": 2.0, "bfe": 2.0}
 
 
@@ -152,6 +161,27 @@ LDS_CYCLES = {
     "pdf_r2": ((64 + 256 + 256 + 128 + 127) * 2 + 4 * 5 * 2 + 16) / 64.0,
 }
 PEAK_LDS_CYCLES_PER_S = 256 * 2.4e9          # one LDS per CU
+
+# The bound the RC4 formats can approach (round 5): neither pipe is full (VALUBusy 0.73, LdsUtil 0.52);
+# each RC4 wave runs ONE dependent chain -- j -> S[j] address -> LDS read -> ... -> the next pair's LDS read -- and a CU
+# holds 9 of them (a 16 KiB S-box per wave, ~152 KiB allocatable: tools/lds_occ.hip).  tools/rc4_ksa_probe.hip `time`
+# runs the product's RC4 work per candidate (R3/R4: one pass = the asm KSA + the early-reject PRGA-2, 20 per candidate;
+# R2: KSA + the 4-byte PRGA) with ONE wave per CU, so nothing queues in front of its LDS reads: the per-wave time is the
+# chain's own latency.  9 chains per CU at that latency is the most this design delivers; the fraction below is how
+# close the product comes (the rest is the 9 waves' mutual queueing on the LDS and the SIMDs).  Measured on MI355X,
+# best of 3 launches of 4,000 passes after a 0.3 s warm-up (profiles/rc4_latency_r05.txt).
+RC4_CHAINS_PER_CU = 9
+RC4_PASSES = {"pdf_r34": 20, "pdf_r3_40": 20, "pdf_r2": 1}
+RC4_PASS_NS_UNLOADED = {"pdf_r34": 8747.7, "pdf_r3_40": 8729.2, "pdf_r2": 8863.0}
+RC4_LATENCY_SOURCE = "profiles/rc4_latency_r05.txt (the shipped --idregs 24 schedule, 1 wave/CU, mean of 2 launches)"
+
+
+def lds_latency_bound(fmt, cus=256):
+    """candidates/s per GPU if each CU ran RC4_CHAINS_PER_CU chains at the unloaded chain latency (None for formats
+    without an RC4 chain)"""
+    if fmt not in RC4_PASS_NS_UNLOADED:
+        return None
+    return cus * RC4_CHAINS_PER_CU * 64 / (RC4_PASSES[fmt] * RC4_PASS_NS_UNLOADED[fmt] * 1e-9)
 
 
 def lds_frac(fmt, cand_per_s):

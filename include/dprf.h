@@ -88,7 +88,10 @@ typedef struct dprf_stats {
                               (their check kernel follows it on the same stream), else = kernel_ms  (ABI 2) */
 } dprf_stats;
 /* kernel_ms / main_kernel_ms are summed over the devices of a multi-device call (device time); wall_ms is
- * the call's wall time.  candidates / launches are totals over the devices. */
+ * the call's wall time.  candidates / launches are totals over the devices.  PDF R2-R4 alternate consecutive
+ * launches between two streams per device, so a launch's event time includes the tail of its neighbour on the other
+ * stream: their kernel_ms sum can exceed the device time (the library's own chunk sizing times those launches from
+ * completion to completion instead). */
 
 /* Per-device record of the last dprf_search_range / dprf_verify_list call on a context (ABI 4): how the shared
  * chunk cursor split the call, so imbalance between devices is visible (the sums above hide it). */

@@ -128,3 +128,14 @@ def test_single_device_policy_is_the_target_time_size(lib):
     assert lib.plan_chunk("odf_aes256", 16400.0, 1 << 40, 1 << 40, 1) == 1 << 22
     assert lib.plan_chunk("odf_aes256", 16400.0, 1000, 1 << 40, 1) == 1000
     assert lib.plan_chunk("no_such_kernel", 1.0, 100, 100, 1) == 0
+
+
+@pytest.mark.parametrize("kernel", ["pdf_r6", "odf_aes256", "pdf_r24", "office_std", "pdf_r5"])
+def test_rounds_stay_within_the_checkpoint_bound(lib, kernel):
+    """R6's 2^25-candidate chunks (~9 s) made multi-GPU rounds ROUND_CHUNKS x 9 s = ~36 s long; a round
+    (the checkpoint and Ctrl-C granularity of range mode) is capped at ROUND_MAX_SECONDS, and the simulated 8-device
+    rounds stay balanced at that length (test above)."""
+    from dprf_amd import brute_force as bf
+    for ndev in (1, 2, 8):
+        for r, rd in enumerate(run_search(lib, kernel, ndev, 4)):
+            assert rd["wall_ms"] <= 1.15 * bf.ROUND_MAX_SECONDS * 1e3, (kernel, ndev, r, rd["wall_ms"])

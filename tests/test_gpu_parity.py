@@ -1,5 +1,6 @@
 """GPU parity: libdprf.so's kernels vs the reference's verdicts (golden fixtures) and vs the oracle, through
 the C ABI.  Bit-exact: hit sets must be identical."""
+import os
 import random
 import tempfile
 import zlib
@@ -92,6 +93,40 @@ def test_long_and_short_lowest_hit_across_sub_lists(dprf, long_verdicts):
         h1, _, _ = c.verify_list(words, stop_on_first=True, cap=1)
         assert h1 == [1717]
         c.close()
+
+
+def test_short_and_long_hits_on_one_document_stop_on_first(dprf, oracle):
+    """a list whose hits sit in BOTH sub-lists of one document -- the ODF -e stream of odt_long_e_200 (its
+    2-byte check, odt...c:98-101, accepts ~2^-16 of all candidates): the 200-byte password is a long hit and
+    tests/golden/make_mixed.py found short candidates the reference verifier also accepts (exit code 1).  Under
+    stop_on_first with cap = 1 the answer is the lowest LIST index whichever sub-list holds it: a short hit below a
+    long one (the long sub-list is then cut to the records below it, dprf_host.cpp dprf_verify_list) and a long hit
+    below a short one; on one device lane and on two.  The fillers are checked with the CPU oracle (a filler the -e
+    check happened to accept would be a hit of its own)."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "mixed_verdicts.json")))
+    octx = oracle.Ctx(d["stream"])
+    rng = random.Random(11)
+    words = []
+    while len(words) < 1500:
+        w = "".join(rng.choice(ALNUM) for _ in range(rng.choice((6, 9, 70, 90))))
+        if octx.verify(w) == 0:
+            words.append(w)
+    short, long_ = d["short_hits"][0], d["long_hit"]
+    for plant in ({300: short, 900: long_}, {300: long_, 900: short}, {300: short, 301: short[::-1], 900: long_}):
+        ws = list(words)
+        for k, v in plant.items():
+            ws[k] = v
+        want = sorted(k for k, v in plant.items() if octx.verify(v) == 1)
+        for devs in ([0], [0, 0]):
+            c = _long_ctx(dprf, d, devs)
+            hits, n, st = c.verify_list(ws)
+            assert hits == want and n == len(want), (plant, devs, hits)
+            h1, n1, st1 = c.verify_list(ws, stop_on_first=True, cap=1)
+            assert h1 == [300], (plant, devs, h1)
+            if plant[300] == short:    # the long records above the short hit are not verified at all
+                assert st1["candidates"] <= len(ws) - sum(1 for w in ws[300:] if len(w.encode()) > 64), (devs, st1)
+            c.close()
 
 
 def test_long_list_over_several_launches(dprf, oracle, long_verdicts):

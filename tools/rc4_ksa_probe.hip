@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(64) k_probe(const uint32_t *keys, uint8_t *out
  * k_pdf_r24's RC4 wave runs it, repeated `passes` times by WPC one-wave workgroups per CU.  With one wave per CU
  * nothing queues in front of a wave's LDS reads: the pass time is the chain's own latency (issue + unloaded round
  * trips), and 9 chains per CU (the S-box capacity) at that latency is the most the KSA design can deliver. */
-template <int NK>
+template <int NK, int R>
 __global__ void __launch_bounds__(64) k_time(const uint32_t *keys, uint32_t *sink, int passes) {
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
     const uint32_t sbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)S);
@@ -64,12 +64,17 @@ __global__ void __launch_bounds__(64) k_time(const uint32_t *keys, uint32_t *sin
 #pragma unroll
         for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
         rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
-        rc4_prga<2>(S, lane << 2, d);
+        if (R == 2) {                      /* R2: one KSA + the 4-byte early-reject PRGA per candidate */
+            uint32_t jj = 0;
+            rc4_prga_span<1, 4>(S, lane << 2, d, jj);
+        } else {
+            rc4_prga<2>(S, lane << 2, d);
+        }
     }
     sink[g] = d[0];
 }
 
-template <int NK>
+template <int NK, int R>
 static void time_passes(int passes) {
     int ncu = 0;
     CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -83,14 +88,14 @@ static void time_passes(int passes) {
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
     /* warm-up: ~0.3 s of full-occupancy work, so the clock has ramped before the first timed launch */
-    for (int r = 0; r < 8; r++) hipLaunchKernelGGL(k_time<NK>, dim3(ncu * 9), dim3(64), 0, 0, dk, ds, passes);
+    for (int r = 0; r < 8; r++) hipLaunchKernelGGL((k_time<NK, R>), dim3(ncu * 9), dim3(64), 0, 0, dk, ds, passes);
     CHECK(hipDeviceSynchronize());
     for (int wpc : {1, 2, 3, 4, 6, 9, 1}) {
         const int blocks = ncu * wpc;
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             CHECK(hipEventRecord(a, 0));
-            hipLaunchKernelGGL(k_time<NK>, dim3(blocks), dim3(64), 0, 0, dk, ds, passes);
+            hipLaunchKernelGGL((k_time<NK, R>), dim3(blocks), dim3(64), 0, 0, dk, ds, passes);
             CHECK(hipEventRecord(b, 0));
             CHECK(hipEventSynchronize(b));
             float ms = 0;
@@ -101,9 +106,9 @@ static void time_passes(int passes) {
         /* candidates/s if every CU ran 9 such chains at this pass time (R3/R4: 20 passes per candidate) */
         const double bound9 = (double)ncu * 9 * 64 / (20.0 * pass_ns * 1e-9);
         const double rate = (double)blocks * 64 / (20.0 * pass_ns * 1e-9);
-        printf("{\"nk\": %d, \"waves_per_cu\": %d, \"cus\": %d, \"passes\": %d, \"ms\": %.3f, \"pass_ns\": %.1f, "
+        printf("{\"r\": %d, \"nk\": %d, \"waves_per_cu\": %d, \"cus\": %d, \"passes\": %d, \"ms\": %.3f, \"pass_ns\": %.1f, "
                "\"group_ns\": %.3f, \"r34_cand_per_s\": %.4g, \"r34_bound_9_chains_at_this_latency\": %.4g}\n",
-               NK, wpc, ncu, passes, best, pass_ns, pass_ns / 128.0, rate, bound9);
+               R, NK, wpc, ncu, passes, best, pass_ns, pass_ns / 128.0, rate, bound9);
     }
     CHECK(hipFree(dk)); CHECK(hipFree(ds));
 }
@@ -180,8 +185,9 @@ int main(int argc, char **argv) {
     if (argc > 1 && !strcmp(argv[1], "time")) {          /* rc4_ksa_probe time [passes] */
         const int passes = argc > 2 ? atoi(argv[2]) : 4000;
         if (passes < 1 || passes > 100000) { printf("bad args\n"); return 2; }
-        time_passes<16>(passes);
-        time_passes<5>(passes);
+        time_passes<16, 3>(passes);
+        time_passes<5, 3>(passes);
+        time_passes<5, 2>(passes);
         return 0;
     }
     const int blocks = argc > 1 ? atoi(argv[1]) : 4608;   /* 2 generations of 9 waves on 256 CUs */
