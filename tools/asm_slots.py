@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Issue-slot cost of a kernel's hottest loop from a hipcc -save-temps .s, with the gfx950 VALU rates
 measured by tools/valu_peak.hip (profiles/valu_issue_rates_r01.txt): full-rate ops 1 slot, half-rate 2,
-v_bitop3 1.7.  Usage: asm_slots.py file.s kernel_regex"""
+v_bitop3 1 (measured full rate, round 5).  Usage: asm_slots.py file.s kernel_regex"""
 import re
 import sys
 from collections import Counter
@@ -9,7 +9,7 @@ from collections import Counter
 FULL = {"v_add_u32", "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_and_b32", "v_or_b32", "v_not_b32",
         "v_lshrrev_b32", "v_ashrrev_i32", "v_lshlrev_b16", "v_mov_b32", "v_add_co_u32", "v_addc_co_u32",
         "v_sub_co_u32", "v_subb_co_u32"}
-HALF_RATE_FACTOR = {"v_bitop3_b32": 1.7}
+HALF_RATE_FACTOR = {"v_bitop3_b32": 1.0}   # full rate unless all three sources share a VGPR bank (round 5: profiles/vgpr_bank_r04.txt)
 
 
 def cost(op):

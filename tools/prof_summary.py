@@ -26,7 +26,9 @@ import sys
 
 SIMDS, XCDS, CUS = 256 * 4, 8, 256
 PASSES = ("fetch", "write", "sq", "lds")
-PMC_STEPS = 1          # tools/profile_gpu.sh: --steps 1 --warmup 0 for every --pmc pass
+PMC_STEPS = 2          # tools/profile_gpu.sh: --steps 2 --warmup 1 for every --pmc pass (round 5: the counted steps
+                       # are the last, at the steady-state launch size -- their dispatches are the last per_step x 2 of
+                       # each pass -- and two of them, so one context-saved dispatch still leaves a clean one)
 
 
 def timed_dispatches(src, bench):
@@ -72,6 +74,11 @@ def summarize(src, dst):
     # kernel -> pass -> counter -> {dispatch: value}
     raw = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(dict)))
     dur = collections.defaultdict(lambda: collections.defaultdict(dict))
+    grid = collections.defaultdict(lambda: collections.defaultdict(dict))
+    roof = (bp or {}).get("roofline") or {}
+    # dispatches of the counted (last) step: the bench's launches per step (kernel-trace pass) x PMC_STEPS
+    per_step = (max(1, round(batch / roof["candidates_per_launch"]))
+                if batch and roof.get("candidates_per_launch") else None)
     for sub in PASSES:
         f = os.path.join(src, sub, sub + "_counter_collection.csv")
         if not os.path.exists(f):
@@ -83,9 +90,25 @@ def summarize(src, dst):
             d = r["Dispatch_Id"]
             raw[k][sub][r["Counter_Name"]][d] = raw[k][sub][r["Counter_Name"]].get(d, 0.0) + float(r["Counter_Value"])
             dur[k][sub][d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            grid[k][sub][d] = int(r.get("Grid_Size") or 0)
     summ = {}
-    for k, passes in raw.items():
+    for k, passes_all in raw.items():
         per = {"per_dispatch": {}, "passes": {}}
+        # round 5: only the counted step's dispatches (the warm-up step before it runs the first, smaller launches)
+        passes = {}
+        for sub, ctrs in passes_all.items():
+            ids = sorted(dur[k][sub], key=int)
+            keep = set(ids[-per_step * PMC_STEPS:] if per_step else ids)
+            passes[sub] = {name: {d: v for d, v in vals.items() if d in keep} for name, vals in ctrs.items()}
+            dur[k][sub] = {d: t for d, t in dur[k][sub].items() if d in keep}
+        # context saves (round 5): a dispatch whose waves were saved and restored counts them twice in
+        # SQ_WAVES, and its HBM bytes include the save of every resident wave's registers and the CUs' LDS (~140-180 MB)
+        saves = {}
+        for sub, ctrs in passes.items():
+            for d, w in ctrs.get("SQ_WAVES", {}).items():
+                g = grid[k][sub].get(d, 0)
+                if g and w > 1.05 * ((g + 63) // 64):
+                    saves.setdefault(sub, []).append(d)
         for sub, ctrs in passes.items():
             avg = {name: sum(v.values()) / len(v) for name, v in ctrs.items()}
             # HBM byte counters (round 4): every dispatch's value is recorded, and per_dispatch holds the MEDIAN dispatch
@@ -95,7 +118,8 @@ def summarize(src, dst):
             # until the rate is measured, then ~2^25, where a median dispatch says nothing per candidate).
             for name in ("FETCH_SIZE", "WRITE_SIZE"):
                 if name in ctrs:
-                    vals = [ctrs[name][d] for d in sorted(ctrs[name], key=int)]
+                    vals = [ctrs[name][d] for d in sorted(ctrs[name], key=int) if d not in saves.get(sub, [])] or \
+                        [ctrs[name][d] for d in sorted(ctrs[name], key=int)]
                     med = sorted(vals)[len(vals) // 2] if len(vals) % 2 else sum(sorted(vals)[len(vals) // 2 - 1:len(vals) // 2 + 1]) / 2
                     avg[name] = med
                     per.setdefault("hbm_dispatch_values", {})[name] = vals
@@ -133,6 +157,12 @@ def summarize(src, dst):
                 per["wait_any_frac"] = pd["SQ_WAIT_ANY"] / pd["SQ_WAVE_CYCLES"]
             if "SQ_WAIT_INST_ANY" in pd:
                 per["wait_inst_any_frac"] = pd["SQ_WAIT_INST_ANY"] / pd["SQ_WAVE_CYCLES"]
+        if saves:
+            per["context_saves"] = {sub: [{"dispatch": d, "sq_waves": passes[sub]["SQ_WAVES"][d],
+                                           "grid_waves": (grid[k][sub][d] + 63) // 64,
+                                           "bytes": {n: passes[sub][n][d] * 1024 for n in ("FETCH_SIZE", "WRITE_SIZE")
+                                                     if d in passes[sub].get(n, {})}} for d in ds]
+                                    for sub, ds in saves.items()}
         if "FETCH_SIZE" in pd or "WRITE_SIZE" in pd:
             # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads 1/2 of wide streaming
             # reads (MI355X_MICROARCH.md HBM section) -- these kernels have no streaming reads, no correction.
@@ -142,22 +172,31 @@ def summarize(src, dst):
                 per["pmc_candidates"] = batch * PMC_STEPS
                 per["hbm_bytes_per_candidate_run_total"] = (tot.get("FETCH_SIZE", 0) + tot.get("WRITE_SIZE", 0)) * 1024 / (
                     batch * PMC_STEPS)
-                # per candidate: the median over dispatches of bytes / that dispatch's candidates, which are estimated as the
-                # run's candidates in proportion to the dispatch's duration (one kernel at a steady rate; the launch sizes
-                # of a run differ).  The run total alone let one first dispatch that wrote 2-3x the others (r03i, r04m: R6
-                # 260,5xx vs 83,2xx KiB at equal size) decide the figure.
-                bpc = 0.0
+                # per candidate (round 5): the counted step's bytes over its candidates, without the dispatches whose
+                # waves were context-saved (their bytes include the save, not kernel traffic); the median over those
+                # dispatches of bytes / that dispatch's candidates (estimated by its share of the step's kernel time) is
+                # kept beside it -- the two agree when the launches are alike
+                bpc, bpc_med, bpc_all = 0.0, 0.0, 0.0
                 for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
                     vals = passes.get(sub, {}).get(name)
                     ds = dur[k].get(sub, {})
                     tdur = sum(ds.get(d, 0) for d in (vals or {}))
                     if not vals or not tdur:
                         continue
-                    pcs = sorted(v * 1024 / (batch * PMC_STEPS * ds[d] / tdur) for d, v in vals.items() if ds.get(d))
-                    m = len(pcs)
-                    med = pcs[m // 2] if m % 2 else (pcs[m // 2 - 1] + pcs[m // 2]) / 2
-                    per.setdefault("hbm_bytes_per_candidate_by_dispatch", {})[name] = pcs
-                    bpc += med
+                    cands = {d: batch * PMC_STEPS * ds[d] / tdur for d in vals if ds.get(d)}
+                    clean = [d for d in cands if d not in saves.get(sub, [])]
+                    bpc_all += sum(vals[d] for d in cands) * 1024 / sum(cands.values())
+                    if not clean:     # every counted dispatch was context-saved: the figure includes the saves
+                        per["hbm_no_clean_dispatch"] = True
+                        clean = list(cands)
+                    if clean:
+                        bpc += sum(vals[d] for d in clean) * 1024 / sum(cands[d] for d in clean)
+                        pcs = sorted(vals[d] * 1024 / cands[d] for d in clean)
+                        m = len(pcs)
+                        bpc_med += pcs[m // 2] if m % 2 else (pcs[m // 2 - 1] + pcs[m // 2]) / 2
+                        per.setdefault("hbm_bytes_per_candidate_by_dispatch", {})[name] = pcs
+                per["hbm_bytes_per_candidate_with_saves"] = bpc_all
+                per["hbm_bytes_per_candidate_median"] = bpc_med
                 per["hbm_bytes_per_candidate"] = bpc
         summ[k] = per
     out["counters"] = summ
