@@ -228,6 +228,76 @@ k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, 
  * and leaves the AES-128 key X1[0:16] of every candidate in HBM ([word][candidate], coalesced);
  * k_office_check does the AES-128 verifier check with its own register budget.  The hand-off costs
  * 32 bytes per candidate against ~3e7 issue slots of hashing. */
+#ifdef OFFICE_KDF_PAIR
+/* round 5 A/B: two candidates per lane (2 g0, 2 g0 + 1), their 50,000 SHA-1s in lockstep (dev_crypto.h
+ * sha1_compress2): two independent instruction streams per lane, at 4 waves/SIMD */
+#define OFFICE_PER 2u
+template <int MODE>
+__global__ void __launch_bounds__(256, 4)
+k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
+    __shared__ uint8_t cs[256];
+    __shared__ uint32_t flag;
+    if (!block_prologue<false, false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag, 2u)) return;
+    const uint32_t g0 = 2u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (g0 >= e.count) return;
+    const uint32_t gg[2] = {g0, g0 + 1u < e.count ? g0 + 1u : g0};
+    uint32_t h[2][5];
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[x][k] = keys[(size_t)k * e.count + gg[x]];
+        } else {
+            cand c;
+            get_candidate<MODE, true>(e, cs, gg[x], c);
+            uint32_t m[32];
+            m[0] = p.salt[0]; m[1] = p.salt[1]; m[2] = p.salt[2]; m[3] = p.salt[3];
+            be_append<4>(m, c);
+            sha1_msg2(m, 16u + c.len, h[x]);
+        }
+    }
+    for (uint32_t i = 0; i < 50000u; i++) {
+        uint32_t w[2][16], s[2][5];
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            const uint32_t m[16] = {bswap32(i), h[x][0], h[x][1], h[x][2], h[x][3], h[x][4], 0x80000000u, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 192u};
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[x][j] = m[j];
+            sha1_iv(s[x]);
+        }
+        sha1_compress2(s, w);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[x][k] = s[x][k];
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t hh[5];
+        {
+            uint32_t w[16] = {h[x][0], h[x][1], h[x][2], h[x][3], h[x][4], 0u, 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 192u};
+            sha1_iv(hh);
+            sha1_compress(hh, w);
+        }
+        uint32_t x1[5];
+        {
+            uint32_t w[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[j] = 0x36363636u ^ (j < 5 ? hh[j] : 0u);
+            sha1_iv(x1);
+            sha1_compress(x1, w);
+            uint32_t w2[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512u};
+            sha1_compress(x1, w2);
+        }
+        if (x == 0 || g0 + 1u < e.count) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) keys[(size_t)k * e.count + gg[x]] = x1[k];
+        }
+    }
+}
+#else
+#define OFFICE_PER 1u
 template <int MODE>
 __global__ void __launch_bounds__(256, 8)
 k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
@@ -280,6 +350,7 @@ k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_o
 #pragma unroll
     for (int k = 0; k < 4; k++) keys[(size_t)k * e.count + g] = x1[k];
 }
+#endif
 
 __global__ void __launch_bounds__(256)
 k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
@@ -363,6 +434,63 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
     }
     /* the midstates' message-independent parts of rounds 0-4, once per candidate (dev_crypto.h sha1_pre) */
     const sha1_pre_t ipre = sha1_pre(ist), opre = sha1_pre(ost);
+#ifdef ODT_KDF_PAIR
+    /* round 5 A/B: both output blocks in one loop, their SHA-1s in lockstep (dev_crypto.h sha1_compress_pre2) */
+    {
+        uint32_t u[2][5], t[2][5];
+        {
+            uint32_t w[2][16], s[2][5];
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                const uint32_t m[16] = {p.salt[0], p.salt[1], p.salt[2], p.salt[3], (uint32_t)(x + 1), 0x80000000u,
+                                        0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[x][j] = m[j];
+            }
+            sha1_compress_pre2(ist, ipre, w, s);
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                const uint32_t m[16] = {s[x][0], s[x][1], s[x][2], s[x][3], s[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
+                                        0, 0, (64u + 20u) * 8u};
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[x][j] = m[j];
+            }
+            sha1_compress_pre2(ost, opre, w, u);
+        }
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) t[x][k] = u[x][k];
+        for (int it = 1; it < 1024; it++) {
+            uint32_t w[2][16], s[2][5];
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                const uint32_t m[16] = {u[x][0], u[x][1], u[x][2], u[x][3], u[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
+                                        0, 0, (64u + 20u) * 8u};
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[x][j] = m[j];
+            }
+            sha1_compress_pre2(ist, ipre, w, s);
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                const uint32_t m[16] = {s[x][0], s[x][1], s[x][2], s[x][3], s[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
+                                        0, 0, (64u + 20u) * 8u};
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[x][j] = m[j];
+            }
+            sha1_compress_pre2(ost, opre, w, u);
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int k = 0; k < 5; k++) t[x][k] ^= u[x][k];
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) keys[(size_t)k * e.count + g] = t[0][k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) keys[(size_t)(5 + k) * e.count + g] = t[1][k];
+    }
+    if (true) return;
+#endif
 #pragma unroll
     for (int blkno = 1; blkno <= 2; blkno++) {
         uint32_t u[5], t[5];
@@ -1008,9 +1136,9 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
-    else if (e.mode == 1) hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
-    else hipLaunchKernelGGL(k_office_kdf<2>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
+    else if (e.mode == 1) hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_office_kdf<2>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();
