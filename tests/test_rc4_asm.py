@@ -1,9 +1,11 @@
 """The generated RC4 key-schedule asm (dprf_amd/csrc/rc4_ksa_asm.h, tools/gen_rc4_ksa_asm.py) executed by a small
 emulator of the gfx950 instructions it uses, for a whole 64-lane wave with its 16 KiB S-box area, against a plain
 RC4 key schedule (RFC 6229's algorithm, the one EVP_rc4 runs for pdf_password_verifier.c:157-176).  This pins the
-schedule's dataflow -- deferred S[i] stores, SDWA byte selects, the [i/4][lane][i%4] layout -- on the CPU; the LDS
-wait placement is checked by construction in the generator (each consumer sits behind an lgkmcnt that covers its
-read) and on the GPU by the parity tests."""
+schedule's dataflow -- deferred S[i] stores, SDWA byte selects, the [i/4][lane][i%4] layout -- on the CPU.  What the
+dataflow emulation cannot see -- LDS results landing only at a covering s_waitcnt, VGPR sources (partial and d16
+destinations included) read at issue, the M0 wait state -- is checked by `lds_hazards` (round 5: it rejects the two
+schedules that were wrong on the MI355X although emulate() passed them, profiles/rc4_ksa_probe_r05.txt), and the
+whole block on the GPU by tools/rc4_ksa_probe.hip and the parity tests."""
 import os
 import random
 import re
