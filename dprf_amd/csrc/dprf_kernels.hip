@@ -1032,7 +1032,20 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
         return;
     }
     /* RC4 wave */
+#ifdef R24_PRIO_SPLIT
+    /* round 5 A/B: the RC4 waves of a CU at R24_PRIO_SPLIT different priorities (3, 2, ... by workgroup), all above the
+     * key waves: under issue contention a chain's rate is 1 / its group latency, and by convexity a spread of latencies
+     * around the same mean serves more groups than equal ones (tools/rc4_probe_pmc.py: at 9 waves per CU 22 % of a chain's
+     * wave-cycles are "ready, not issued") */
+    {
+        const uint32_t lvl = blockIdx.x % (uint32_t)R24_PRIO_SPLIT;
+        if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+    }
+#else
     __builtin_amdgcn_s_setprio(R24_PRIO);
+#endif
     uint8_t *Sw = S;
     /* the asm KSA needs the S-box area at an LDS address with zero low 16 bits (rc4_ksa_asm); S is this kernel's
      * first LDS object, at 0 -- checked, and a launch that ever breaks it fails loudly instead of computing wrong */

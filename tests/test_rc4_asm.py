@@ -159,7 +159,8 @@ def emulate(prog, keys, nk, sbase=0, text=None):
         elif op == "v_cmp_eq_u32_sdwa":
             assert "src0_sel:BYTE_0" in ln
             src1 = a[2].split()[0]
-            if src1.startswith("%") and src1 not in sregs and (src1 not in vin or not isinstance(vin[src1], int)):
+            if (src1.startswith("%") or re.match(r"v\d+$", src1)) and src1 not in sregs and \
+                    (src1 not in vin or not isinstance(vin[src1], int)):
                 # a VGPR, byte-selected (BYTE_3 of j: the position counter; BYTE_2/3 of the ic4 constants)
                 sh1 = {"BYTE_0": 0, "BYTE_1": 8, "BYTE_2": 16, "BYTE_3": 24}[re.search(r"src1_sel:(\w+)", ln).group(1)]
                 r = (v(a[1]) & np.uint64(0xff)) == ((v(src1) >> np.uint64(sh1)) & np.uint64(0xff))
@@ -170,7 +171,8 @@ def emulate(prog, keys, nk, sbase=0, text=None):
             else:
                 masks[a[0]] = r
         elif op == "ds_read_u8":
-            regs[a[0]] = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
+            base, o = a[1].split()[0], off(a[1].split()[1] if len(a[1].split()) > 1 else None)
+            regs[a[0]] = lds[(v(base) + np.uint64(o)).astype(np.int64)].astype(np.uint64)
         elif op in ("ds_read_u8_d16", "ds_read_u8_d16_hi"):
             b = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
             old = regs.get(a[0], np.zeros(LANES, dtype=np.uint64))
@@ -187,7 +189,8 @@ def emulate(prog, keys, nk, sbase=0, text=None):
                 r |= byte << np.uint64(8 * k)
             regs[a[0]] = r
         elif op == "ds_write_b8":
-            lds[v(a[0]).astype(np.int64)] = (v(a[1]) & np.uint64(0xff)).astype(np.uint8)
+            d, o = a[1].split()[0], off(a[1].split()[1] if len(a[1].split()) > 1 else None)
+            lds[(v(a[0]) + np.uint64(o)).astype(np.int64)] = (v(d) & np.uint64(0xff)).astype(np.uint8)
         elif op == "ds_write_b128":
             assert a[1].split()[0] == "v[60:63]"
             o = off(a[1].split()[1]) if len(a[1].split()) > 1 else 0
@@ -292,7 +295,7 @@ def lds_hazards(prog):
 
 @pytest.mark.parametrize("flag", ["", "--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
                                   "--jctr", "--early-v1", "--ic4", "--split-add", "--split-add --ic4", "--and-or",
-                                  "--idregs 24", "--mskor"])
+                                  "--idregs 24", "--mskor", "--bytes"])
 def test_schedule_waits_cover_every_lds_result(flag):
     """Every schedule the GPU ran green reads an LDS result only after an lgkmcnt wait that covers it."""
     import subprocess
@@ -356,7 +359,7 @@ def test_generated_ksa_equals_rc4(nk):
 
 
 @pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add", "--mskor",
+                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add", "--mskor", "--bytes",
                                   "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or", "--idregs 24"])
 def test_schedule_variants_equal_rc4(flag):
     """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this

@@ -53,6 +53,9 @@ Usage: tools/gen_rc4_ksa_asm.py > dprf_amd/csrc/rc4_ksa_asm.h
                                                                     rate, as before round 4; default: v_bitop3_b32)
        tools/gen_rc4_ksa_asm.py --mskor > <variant header>          (round 5 A/B: S[j] read + store as one
                                                                     ds_mskor_rtn_b32: 4 LDS ops per group, 18 VALU)
+       tools/gen_rc4_ksa_asm.py --bytes > <variant header>          (round 5 A/B: the S[i] pair as two byte loads /
+                                                                    stores, full-rate selects: 36 VALU cycles per
+                                                                    group instead of 40, 8 LDS ops instead of 6)
        tools/gen_rc4_ksa_asm.py --idregs 24 [--no-m0-wait] > <hdr>  (round 4 A/B: identity rows 0-23 from input VGPRs;
                                                                     --no-m0-wait: round 4's first, wrong, schedule)
        tools/gen_rc4_ksa_asm.py --b128-identity > <variant header>  (A/B: the identity as 16 ds_write_b128 + 30
@@ -359,6 +362,67 @@ def ksa_mskor(nk):
     return out
 
 
+def ksa_bytes(nk, idregs=0):
+    """Round 5 A/B (--bytes): the S[i] pair of a group as two BYTE registers (two ds_read_u8 instead of one u16 read) and
+    stored back as two bytes, so the select of v1 and the two merge selects are full-rate `v_cndmask_b32_e32` instead of
+    half-rate SDWA forms: 6 half-rate + 6 full-rate VALU per group (36 VALU cycles) instead of 8 + 4 (40), for 8 LDS
+    operations instead of 6.  Why: under load a chain's extra latency is issue contention (tools/rc4_probe_pmc.py: 22 %
+    of wave-cycles ready-not-issued at 9 waves per CU), which the SIMD time of the half-rate ops drives."""
+    J, W, X0, X1, V1, A0, A1, M, ST, M0S, WN, C0, C1, C2, C3, H0, LB, SB, IA, C16, D0 = (
+        "%%%d" % k for k in range(21))
+    KB = ["%%%d" % (21 + k) for k in range(nk)]
+    W0, W1, M1 = W, WN, "v60"          # W1 in the IC-free register of the vconst schedule's WN; M1 a clobbered VGPR
+    IC = "v61"                         # the compare constants (i0, i1) in bytes 0, 1 (clobbered VGPR)
+    out = []
+    e = out.append
+    identity(e, M, M0S, SB, ["%%%d" % (21 + nk + k) for k in range(idregs)])
+    e("v_mov_b32 %s, 0" % J)
+    e("v_mov_b32 %s, 0" % W0)          # S[0], S[1] of the identity
+    e("v_mov_b32 %s, 1" % W1)
+    FIRST_IC = 32
+    e("v_mov_b32 %s, 0x%x" % (IC, (2 * FIRST_IC) | ((2 * FIRST_IC + 1) << 8)))
+
+    def cmp(i, sel):
+        if q < FIRST_IC:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %d src0_sel:BYTE_0 src1_sel:DWORD" % (J, i))
+        else:
+            e("v_cmp_eq_u32_sdwa vcc, %s, %s src0_sel:BYTE_0 src1_sel:%s" % (J, IC, sel))
+
+    for q in range(128):
+        i0, i1 = 2 * q, 2 * q + 1
+        if q > 0:
+            e("s_waitcnt lgkmcnt(2)")          # W0, W1 landed; the previous group's two S[i] stores may be in flight
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, W0, KB[i0 % nk]))
+        e(addr_lo(A0, J, LB, True))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A0, J))
+        cmp(i1, "BYTE_1")
+        e("ds_read_u8 %s, %s" % (X0, A0))
+        e("ds_write_b8 %s, %s" % (A0, W0))
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (V1, W1, W0))        # v1 = hit1 ? S[i0] : S[i1]
+        e("v_add3_u32 %s, %s, %s, %s" % (J, J, V1, KB[i1 % nk]))
+        e(addr_lo(A1, J, LB, True))
+        e("v_lshrrev_b32_sdwa %s, 2, %s dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0"
+          % (A1, J))
+        cmp(i0, "BYTE_0")
+        e("ds_read_u8 %s, %s" % (X1, A1))
+        e("ds_write_b8 %s, %s" % (A1, V1))
+        if FIRST_IC <= q < 127:
+            e("v_add_u32 %s, 0x202, %s" % (IC, IC))
+        if q < 127:
+            e("ds_read_u8 %s, %s offset:%d" % (W0, LB, pos(i0 + 2)))
+            e("ds_read_u8 %s, %s offset:%d" % (W1, LB, pos(i0 + 3)))
+            e("s_waitcnt lgkmcnt(2)")          # x0, x1 landed (the next pair may still be in flight)
+        else:
+            e("s_waitcnt lgkmcnt(0)")
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M, X0, V1))         # S[i0] = hit0 ? v1 : x0
+        e("v_cndmask_b32_e32 %s, %s, %s, vcc" % (M1, X1, X0))        # S[i1] = hit0 ? x0 : x1
+        e("ds_write_b8 %s, %s offset:%d" % (LB, M, pos(i0)))
+        e("ds_write_b8 %s, %s offset:%d" % (LB, M1, pos(i1)))
+    e("s_waitcnt lgkmcnt(0)")
+    return out
+
+
 def identity(e, M, M0S, SB, ids=(), m0_wait=True):
     """ids (round 4 A/B, --idregs N): input VGPRs holding rows 0..N-1 of the identity (loop-invariant constants the
     kernel keeps in registers), so only the rows after them need the add chain"""
@@ -512,6 +576,7 @@ def main():
         print("#define RC4_KSA_SELNOHIT 0x0c0c0604u")
     for nk in KEYLENS:
         lines = (ksa_early_v1(nk) if "--early-v1" in sys.argv else ksa_mskor(nk) if "--mskor" in sys.argv else
+                 ksa_bytes(nk, idregs) if "--bytes" in sys.argv else
                  ksa(nk, early, late, pre, vconst and not early, b128, jctr, ic4, d16, split, b3addr, idregs,
                      "--no-m0-wait" not in sys.argv))
         print("#define RC4_KSA_ASM_%d \\" % nk)
