@@ -107,3 +107,21 @@ def test_lds_instruction_count_matches_rocprof():
         measured = pd["SQ_INSTS_LDS"] / pd["SQ_WAVES"] * 2
         model = per_batch[fmt] * batches[fmt]
         assert abs(measured - model) / model < 0.01, (fmt, measured, model)
+
+
+def test_cost_table_and_latency_bound():
+    """Round 5: v_bitop3 at its measured full rate (profiles/vgpr_bank_r04.txt), the floors that follow,
+    the spec ops beside them, and the R2-R4 chain-latency bound bench.py quotes those formats against."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    assert work.COST["bitop3"] == 1.0
+    assert round(work.per_candidate("odt", part="main")) == 3899518          # 4,094 HMAC SHA-1c + 4 + 1 SHA-256c
+    assert round(work.per_candidate("odt", "spec", part="main")) == 2296 + 4098 * 1001
+    b = work.lds_latency_bound("pdf_r34")
+    assert abs(b - 256 * 9 * 64 / (20 * work.RC4_PASS_NS_UNLOADED["pdf_r34"] * 1e-9)) < 1
+    assert 7.0e8 < b < 1.0e9 and 1.4e10 < work.lds_latency_bound("pdf_r2") < 2.0e10
+    assert work.lds_latency_bound("odt") is None and bench.latency_roof("odt", 1e7) is None
+    r = bench.latency_roof("pdf_r34", 0.745 * b)
+    assert r["bound_cand_per_s"] == b and abs(r["frac"] - 0.745) < 1e-9 and r["chains_per_cu"] == 9
