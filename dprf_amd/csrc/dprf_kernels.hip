@@ -76,11 +76,12 @@ DEVI void get_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand 
  * stop flag would let a late-dispatched lower block skip itself).  `per` = candidates per thread.
  * COUNT: this kernel's skipped blocks are counted in R->skipped (the verifying kernel of a format; the
  * KDF kernels of Office/ODF skip exactly the blocks their check kernel skips and do not count). */
-template <bool AES, bool COUNT = true>
+template <bool AES, bool COUNT = true, bool STAGE_CS = true>
 DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_results *R, uint32_t stop_on_first,
                          uint8_t *cs, aes_lds *L, uint32_t *flag, uint32_t per = 1) {
     const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < 64; k += blockDim.x) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
+    if (STAGE_CS)
+        for (uint32_t k = tid; k < 64; k += blockDim.x) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     if (AES) {
         for (uint32_t k = tid; k < 256; k += blockDim.x) { L->te[k] = T->te0[k]; L->td[k] = T->td0[k]; }
         for (uint32_t k = tid; k < 64; k += blockDim.x) {
@@ -954,6 +955,11 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
 #ifndef R24_PRIO
 #define R24_PRIO 3
 #endif
+/* 1: charset, PAD and the skip flag in an LDS area beside the S-boxes (16,720 B per workgroup, 9 per CU); 0: the
+ * S-box area is all the LDS a workgroup takes (16,384 B, 10 per CU) */
+#ifndef R24_LDS_AUX
+#define R24_LDS_AUX 1
+#endif
 /* 1: the KSA as the generated asm block (rc4_dev.h rc4_ksa_asm); 0: the C++ rc4_ksa (A/B builds) */
 #ifndef R24_KSA_ASM
 #define R24_KSA_ASM 1
@@ -983,6 +989,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     constexpr uint32_t NBAT = r24_batches<R>::v;
     static_assert(NBAT % 2 == 0, "block_prologue counts NBAT / 2 candidates per thread of the 128-thread block");
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
+#if R24_LDS_AUX
     __shared__ __attribute__((aligned(16))) uint32_t aux[64 + 16 + 4];
     uint8_t *cs = (uint8_t *)aux;                         /* charset, 256 B */
     uint32_t *padw = aux + 64;                            /* PAD || PAD */
@@ -990,6 +997,15 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
     /* per = candidates per thread of the 128-thread block: 64 * NBAT candidates */
     if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag, NBAT / 2)) return;
+#else
+    /* the S-box area is the workgroup's only LDS (16,384 B: 10 workgroups per 160 KiB CU); the key wave reads the
+     * charset and PAD from the kernel arguments, and the skip flag passes through the S-box area before the first
+     * batch barrier (every wave reads it before that barrier, the key wave writes keys only after it) */
+    const uint8_t *cs = e.charset;
+    const uint32_t *padw = p.pad;
+    uint32_t *flag = (uint32_t *)S;
+    if (!block_prologue<false, true, false>(e, nullptr, R_, stop_on_first, nullptr, nullptr, flag, NBAT / 2)) return;
+#endif
     const uint32_t base = blockIdx.x * (64u * NBAT);
     const uint32_t left = e.count - base;                 /* > 0: grid = ceil(count / (64 * NBAT)) */
     const uint32_t nb = left >= 64u * NBAT ? (uint32_t)NBAT : (left + 63u) / 64u;

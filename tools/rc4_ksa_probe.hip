@@ -83,14 +83,14 @@ static void time_passes(int passes) {
     for (auto &w : keys) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; w = (uint32_t)st; }
     uint32_t *dk, *ds;
     CHECK(hipMalloc(&dk, keys.size() * 4));
-    CHECK(hipMalloc(&ds, (size_t)ncu * 9 * 64 * 4));
+    CHECK(hipMalloc(&ds, (size_t)ncu * 10 * 64 * 4));
     CHECK(hipMemcpy(dk, keys.data(), keys.size() * 4, hipMemcpyHostToDevice));
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
     /* warm-up: ~0.3 s of full-occupancy work, so the clock has ramped before the first timed launch */
     for (int r = 0; r < 8; r++) hipLaunchKernelGGL((k_time<NK, R>), dim3(ncu * 9), dim3(64), 0, 0, dk, ds, passes);
     CHECK(hipDeviceSynchronize());
-    for (int wpc : {1, 2, 3, 4, 6, 9, 1}) {
+    for (int wpc : {1, 2, 3, 4, 6, 8, 9, 10, 1}) {   /* 10: 160 KiB of S-boxes, every byte of the CU's LDS */
         const int blocks = ncu * wpc;
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
