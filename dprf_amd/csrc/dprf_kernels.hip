@@ -767,8 +767,16 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
 /* ================================================================== PDF R5 (one SHA-256) */
 /* One SHA-256 per candidate is ~2,300 cycles of a wave: with one candidate per thread, wave launch and
  * the block prologue were a third of the kernel (2 Mi waves per 128 Mi-candidate launch).  Each thread
- * now takes R5_PER candidates, 256 apart. */
-#define R5_PER 8
+ * takes PER candidates: a run of PER consecutive indices in range mode when the charset has at least PER
+ * characters (PER 16, or 8 for 8-15 characters: one wrap of the last digit per run at most), else -- and in
+ * list mode -- PER candidates 256 apart. */
+/* 1: range-mode threads take runs of consecutive candidates (below); 0: PER candidates 256 apart (A/B) */
+#ifndef R5_RUNS
+#define R5_RUNS 1
+#endif
+#ifndef R5_PER_MAX
+#define R5_PER_MAX 16
+#endif
 /* SHA-256 of one block from the IV, compared with u[0:8], with an early exit: the last word of the digest
  * is IV7 + (e after round 60) -- that e only moves down to h in rounds 61-63 -- so a wave none of whose
  * lanes matches u[7] there (all but a 2^-32 fraction) skips rounds 61-63 and their schedule words. */
@@ -793,13 +801,24 @@ DEVI bool sha256_block_matches(uint32_t w[16], const uint32_t u[8], bool valid) 
            d + 0xa54ff53au == u[3] && e + 0x510e527fu == u[4] && f + 0x9b05688cu == u[5] &&
            g + 0x1f83d9abu == u[6] && h + 0x5be0cd19u == u[7];
 }
-template <int MODE>
-__global__ void __launch_bounds__(256)
+/* NW (range mode): message words 0..NW-1 carry candidate bytes (NW = ceil(pwlen / 4), one instantiation per launch
+ * length); the words after them are the launch-uniform tail alone, so the compiler keeps them, K + W of their rounds
+ * and the schedule terms built only from them in SGPRs (the scalar unit) instead of spending VALU slots on them */
+/* minimum waves per SIMD the register allocation must allow.  Measured (round 5, profiles/ab_r5_runs_r05q.txt,
+ * -pr 7 alnum, three alternating rounds): no bound (132 VGPRs, 3 waves) 32.0 G with runs of 8; 4 waves 32.86 G,
+ * 5 waves 32.95 G with runs of 16 */
+#ifndef R5_WAVES
+#define R5_WAVES 5
+#endif
+template <int MODE, int NW, int PER>
+__global__ void __launch_bounds__(256, R5_WAVES)
 k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t stop_on_first) {
+    static_assert(NW >= 1 && NW <= DPRF_MAX_RANGE_LEN / 4, "candidate words");
+    static_assert(PER == 8 || PER == 16, "run length");
     __shared__ uint8_t cs[256];
     __shared__ uint32_t flag;
-    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag, R5_PER)) return;
-    const uint32_t base = blockIdx.x * (blockDim.x * R5_PER);
+    if (!block_prologue<false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag, PER)) return;
+    const uint32_t base = blockIdx.x * (blockDim.x * PER);
     /* Range mode: every candidate has length pwlen <= DPRF_MAX_RANGE_LEN, so the message is one block and
      * its tail -- salt8 || 0x80 at byte pwlen, the bit length in word 15 -- is the same for the whole
      * launch: 16 uniform BE words built once (SGPRs), OR-ed onto the candidate's BE words. */
@@ -823,8 +842,54 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
         for (int j = 0; j < 15; j++) tail[j] = bswap32(tail[j]);
         tail[15] = (len + 8u) * 8u;
     }
+    if (MODE == 0 && R5_RUNS && e.cslen >= PER) {
+        /* Runs (round 5): thread t takes the PER consecutive indices base + PER t + k, which differ only in the last
+         * character except across one wrap of the last digit (cslen >= PER).  The candidate is spelled twice
+         * per run -- at its first index (last digit d0) and at the first index past the wrap (last digit 0, prefix + 1)
+         * -- as BE message words with the tail already OR-ed in and the last character cleared; each candidate then
+         * costs a select per word and one charset byte instead of a full mixed-radix spelling. */
+        const uint32_t g0 = base + threadIdx.x * PER;
+        const uint32_t gc = g0 < e.count ? g0 : e.count - 1u;
+        const uint32_t lp = e.pwlen - 1u;                             /* position of the last character */
+        const uint32_t lw = lp >> 2, lsh = 24u - 8u * (lp & 3u);      /* its BE word and bit offset */
+        const uint32_t q0 = e.cslen == 1 ? gc : fastdiv(gc, e.div_m, e.div_s);
+        uint32_t d0 = (uint32_t)e.sdig[lp] + (gc - q0 * e.cslen);
+        d0 -= d0 >= e.cslen ? e.cslen : 0u;
+        uint32_t w0[NW], w1[NW];
+        {
+            cand c;
+            range_candidate<false>(e, cs, gc, c);
+#pragma unroll
+            for (int j = 0; j < NW; j++) w0[j] = bswap32(c.w[j]) | tail[j];
+            range_candidate<false>(e, cs, gc + (e.cslen - d0), c);
+#pragma unroll
+            for (int j = 0; j < NW; j++) w1[j] = bswap32(c.w[j]) | tail[j];
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                const uint32_t m = (uint32_t)j == lw ? ~(0xffu << lsh) : ~0u;
+                w0[j] &= m; w1[j] &= m;
+            }
+        }
 #pragma unroll 1
-    for (uint32_t k = 0; k < R5_PER; k++) {
+        for (uint32_t k = 0; k < (uint32_t)PER; k++) {
+            if (base + k >= e.count) break;                             /* uniform: a wave's runs start >= base */
+            const uint32_t g = g0 + k;
+            const bool valid = g < e.count;
+            const uint32_t d = d0 + k;
+            const bool lo = d < e.cslen;
+            const uint32_t ch = (uint32_t)cs[lo ? d : d - e.cslen] << lsh;
+            uint32_t b[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                b[j] = j < NW ? (lo ? w0[j] : w1[j]) : tail[j];
+                if (j < NW && (uint32_t)j == lw) b[j] |= ch;
+            }
+            if (sha256_block_matches(b, p.u, valid)) report_hit(R, e.start + g, cap, stop_on_first);
+        }
+        return;
+    }
+#pragma unroll 1
+    for (uint32_t k = 0; k < (uint32_t)PER; k++) {
         const uint32_t g0 = base + k * blockDim.x + threadIdx.x;
         if (base + k * blockDim.x >= e.count) break;                 /* uniform */
         const bool valid = g0 < e.count;
@@ -835,7 +900,7 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
             /* range_candidate leaves the bytes past pwlen zero */
             uint32_t b[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) b[j] = (j < DPRF_MAX_RANGE_LEN / 4 ? bswap32(c.w[j]) : 0u) | tail[j];
+            for (int j = 0; j < 16; j++) b[j] = (j < NW ? bswap32(c.w[j]) : 0u) | tail[j];
             if (sha256_block_matches(b, p.u, valid)) report_hit(R, e.start + g, cap, stop_on_first);
             continue;
         }
@@ -1198,8 +1263,21 @@ hipError_t launch_long_prehash(const dprf_enum &e, const dprf_long_params &lp, d
 #ifdef DPRF_PART_PDF
 hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,
                          uint32_t stop, hipStream_t s) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_pdf_r5<0>, GRID(e.count, 256 * R5_PER), dim3(256), 0, s, e, p, R, cap, stop);
-    else hipLaunchKernelGGL(k_pdf_r5<1>, GRID(e.count, 256 * R5_PER), dim3(256), 0, s, e, p, R, cap, stop);
+#define L5(M, NW, PER) hipLaunchKernelGGL((k_pdf_r5<M, NW, PER>), GRID(e.count, 256 * PER), dim3(256), 0, s, e, p, R, cap, stop)
+#define L5W(NW) do { if (R5_PER_MAX >= 16 && e.cslen >= 16) L5(0, NW, 16); else L5(0, NW, 8); } while (0)
+    if (e.mode == 0) {
+        switch ((e.pwlen + 3u) >> 2) {
+        case 0: case 1: L5W(1); break;
+        case 2: L5W(2); break;
+        case 3: L5W(3); break;
+        case 4: L5W(4); break;
+        default: L5W(8); break;
+        }
+    } else {
+        L5(1, 8, 8);
+    }
+#undef L5W
+#undef L5
     return hipGetLastError();
 }
 hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_results *R, uint32_t cap,

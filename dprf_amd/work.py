@@ -68,6 +68,44 @@ def sha256_floor():
     return 64 * rnd + 48 * sched + 8 * COST["add"]
 
 
+def sha256_dataflow(var_words, rounds=64, unit="floor"):
+    """Work of one SHA-256 compression from the IV whose message words `var_words` vary per lane and whose other
+    words are wave-uniform (held and combined in SGPRs by the scalar unit, free for the VALU), computing rounds
+    0..rounds-1 and the schedule words they use.  Only operations with a per-lane input count.  unit "spec": the
+    SURVEY 8(d) accounting (every 2-input op, rotate and shift 1: Sigma 5, Ch 4, Maj 5, sigma 5, 26 per round,
+    13 per schedule word, 2,296 for the whole compression with its 8 final additions); unit "floor": issue slots
+    with the COST table (Sigma = 3 rotates + bitop3, sigma = 2 rotates + shift + bitop3, Ch / Maj one bitop3).
+    With rounds < 64 the final additions are the one compare word's (k_pdf_r5's early reject after round 60)."""
+    if unit == "spec":
+        big_s, ch, maj, small_s, add = 5, 4, 5, 5, 1
+    else:
+        big_s = 3 * COST["rot"] + COST["bitop3"]
+        ch = maj = COST["bitop3"]
+        small_s = 2 * COST["rot"] + COST["shr"] + COST["bitop3"]
+        add = COST["add"]
+
+    def adds(n_var, n_other):
+        return 0 if n_var == 0 else (n_var - 1 + (1 if n_other else 0)) * add
+
+    w = [i in var_words for i in range(16)]
+    work = 0.0
+    for t in range(16, rounds):
+        terms = [w[t - 2], w[t - 7], w[t - 15], w[t - 16]]
+        work += (small_s if w[t - 2] else 0) + (small_s if w[t - 15] else 0) + adds(sum(terms), 4 - sum(terms))
+        w.append(any(terms))
+    a, b, c, d, e, f, g, h = [False] * 8          # the IV: constants
+    for t in range(rounds):
+        t1_var = [h, e, e or f or g, w[t]]        # h, Sigma1(e), Ch(e,f,g), W[t]  (+ K: a constant)
+        work += (big_s if e else 0) + (ch if (e or f or g) else 0) + adds(sum(t1_var), 1)
+        t1 = any(t1_var)
+        t2 = a or b or c
+        work += (big_s if a else 0) + (maj if t2 else 0) + (add if a and t2 else 0)
+        work += add if (d or t1) else 0            # e' = d + t1
+        work += add if (t1 or t2) else 0           # a' = t1 + t2
+        h, g, f, e, d, c, b, a = g, f, e, (d or t1), c, b, a, (t1 or t2)
+    return work + (8 if rounds == 64 else 1) * add
+
+
 def sha512_floor():
     add64, rot64, shr64, x64 = 2 * COST["add"], 2 * COST["rot"], COST["rot"] + COST["shr"], 2 * COST["bitop3"]
     rnd = (3 * rot64 + x64) + x64 + 4 * add64 + (3 * rot64 + x64) + x64 + 2 * add64 + add64
@@ -103,6 +141,12 @@ FLOOR = {
     "rc4_ksa": 256 * (2 * COST["add"] + COST["and"] + COST["shl"] + COST["or"]) + 64 * COST["add"],
     "rc4_prga_byte": 2 * COST["add"] + 2 * (COST["and"] + COST["shl"] + COST["or"]) + COST["shl"] + COST["xor"],
 }
+# PDF R5 at its bench configuration (-pr 7: message words 0-1 carry the candidate, 2-15 are launch-uniform salt,
+# padding and length; the compare of IV7 + e after round 60 rejects all but 2^-32 of the candidates): the dataflow
+# floor of the early-reject compression (1,925 slots, against 2,200 for a compression of 16 per-lane words).
+FLOOR["sha256c_r5"] = sha256_dataflow({0, 1}, rounds=61)
+# the floor a format's kernel is held to where its primitive runs on fewer per-lane inputs than the generic one
+FLOOR_AS = {"pdf_r5": {"sha256c": "sha256c_r5"}}
 SPEC = {
     "sha1c": 1001, "sha1c_office_loop": 1001, "sha1c_hmac20": 1001, "sha256c": 2296, "sha512c": 5840,
     "md5c": 532, "md5c_16": 532, "md5c_5": 532, "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
@@ -197,4 +241,5 @@ def per_candidate(fmt, unit="floor", part="all"):
     the dominant kernel's share (MAIN)."""
     table = FLOOR if unit == "floor" else SPEC
     counts = MAIN.get(fmt, COUNTS[fmt]) if part == "main" else COUNTS[fmt]
-    return sum(table[k] * v for k, v in counts.items())
+    alias = FLOOR_AS.get(fmt, {}) if unit == "floor" else {}
+    return sum(table[alias.get(k, k)] * v for k, v in counts.items())

@@ -125,3 +125,20 @@ def test_cost_table_and_latency_bound():
     assert work.lds_latency_bound("odt") is None and bench.latency_roof("odt", 1e7) is None
     r = bench.latency_roof("pdf_r34", 0.745 * b)
     assert r["bound_cand_per_s"] == b and abs(r["frac"] - 0.745) < 1e-9 and r["chains_per_cu"] == 9
+
+
+def test_sha256_dataflow_floor():
+    """The SHA-256 dataflow count (round 5): with every message word per-lane it reproduces SURVEY 8(d)'s 26 spec ops
+    per round and 13 per schedule word (the constant IV folds a few ops out of the first rounds), and the generic
+    floor's 23 + 15 slots; PDF R5's kernel is held to the early-reject compression of its bench configuration
+    (words 0-1 per lane, rounds 0-60), while the spec stays SURVEY's 2,296."""
+    full = set(range(16))
+    for unit, per_round in (("spec", 26 + 13), ("floor", 23 + 15)):
+        # round 63 + schedule word 63 + the 8 final additions instead of the early reject's one
+        assert work.sha256_dataflow(full, 64, unit) - work.sha256_dataflow(full, 63, unit) == per_round + 7
+    assert work.sha256_dataflow(full, 64, "spec") <= 2296 and work.sha256_dataflow(full, 64) <= work.FLOOR["sha256c"]
+    r5 = work.sha256_dataflow({0, 1}, 61)
+    assert work.FLOOR["sha256c_r5"] == r5 and work.per_candidate("pdf_r5") == r5 < work.FLOOR["sha256c"]
+    assert work.per_candidate("pdf_r5", "spec") == 2296
+    # uniform words only remove work, never add it
+    assert work.sha256_dataflow({0}, 61) <= r5 <= work.sha256_dataflow(set(range(8)), 61)
