@@ -30,6 +30,9 @@ if [ -n "$REHEARSE" ]; then
   echo "== rehearsals $(date +%T)"
   DPRF_BENCH_SAME_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --no-side --cpu-seconds 0 --steps 3 > gpurun_out/bench_lanes2_$TAG.json 2> gpurun_out/bench_lanes2_$TAG.err || { tail -20 gpurun_out/bench_lanes2_$TAG.err; exit 1; }
   DPRF_BENCH_SAME_DEVICE=1 DPRF_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_n2_rehearsal_$TAG.json 2> gpurun_out/bench_n2_rehearsal_$TAG.err || { tail -20 gpurun_out/bench_n2_rehearsal_$TAG.err; exit 1; }
-  python -c "import json; [print(f, json.loads(open('gpurun_out/'+f).read().strip().splitlines()[-1])['value']) for f in ('bench_lanes2_$TAG.json', 'bench_n2_rehearsal_$TAG.json')]"
+  # and the RCCL branch the driver's N>1 runs take (one rank, so RCCL accepts it): process group, barriers and the
+  # MIN / MAX all-reduces on device tensors
+  DPRF_BENCH_FORCE_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-side > gpurun_out/bench_rccl1_rehearsal_$TAG.json 2> gpurun_out/bench_rccl1_rehearsal_$TAG.err || { tail -20 gpurun_out/bench_rccl1_rehearsal_$TAG.err; exit 1; }
+  python -c "import json; [print(f, json.loads(open('gpurun_out/'+f).read().strip().splitlines()[-1])['value']) for f in ('bench_lanes2_$TAG.json', 'bench_n2_rehearsal_$TAG.json', 'bench_rccl1_rehearsal_$TAG.json')]"
 fi
 echo "== done $(date +%T)"
