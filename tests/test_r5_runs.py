@@ -114,11 +114,18 @@ def test_r5_runs_find_the_password_at_every_run_position(cs, pw):
     idx = index_of(pw, cs)
     space = len(cs) ** n
     with tempfile.TemporaryDirectory() as t:
-        with _lib.Context(_fields(_stream(t, pw)), device=0) as ctx:
-            for start, count, inside in windows(idx, space, per(cs)):
-                hits, nh, st = ctx.search_range(cs, n, start, count)
-                assert st["candidates"] == count, (pw, start, count)
-                assert hits == ([idx] if inside else []) and nh == len(hits), (pw, start, count, hits)
-                if inside:
-                    fh, _, _ = ctx.search_range(cs, n, start, count, stop_on_first=True, cap=1)
-                    assert fh == [idx], (pw, start, count)
+        fields = _fields(_stream(t, pw))
+    with _lib.Context(fields, device=0) as ctx:
+        for start, count, inside in windows(idx, space, per(cs)):
+            hits, nh, st = ctx.search_range(cs, n, start, count)
+            assert st["candidates"] == count, (pw, start, count)
+            assert hits == ([idx] if inside else []) and nh == len(hits), (pw, start, count, hits)
+            if inside:
+                fh, _, _ = ctx.search_range(cs, n, start, count, stop_on_first=True, cap=1)
+                assert fh == [idx], (pw, start, count)
+    # two device lanes on the one GPU: the call is cut into chunks, each launch's runs start at its own chunk start
+    with _lib.Context(fields, devices=[0, 0]) as ctx:
+        big = max(0, min(idx - (1 << 23) - 3, space - (1 << 24)))         # 2^24 indices: chunks on both lanes
+        for start, count, inside in windows(idx, space, per(cs))[-8:] + [(big, min(1 << 24, space - big), True)]:
+            hits, _, st = ctx.search_range(cs, n, start, count)
+            assert st["candidates"] == count and hits == ([idx] if inside else []), (pw, start, count, hits)
