@@ -30,12 +30,12 @@ __global__ void __launch_bounds__(256) kmask(unsigned *out, unsigned seed) {
 }
 
 template <int OP>
-__global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed) {
+__global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed, int iters = ITERS) {
     unsigned x[CHAINS];
     unsigned y = seed ^ threadIdx.x, z = seed * 3u + blockIdx.x;
 #pragma unroll
     for (int c = 0; c < CHAINS; c++) x[c] = seed + c * 77u + threadIdx.x;
-    for (int i = 0; i < ITERS; i++) {
+    for (int i = 0; i < iters; i++) {
 #pragma unroll
         for (int c = 0; c < CHAINS; c++) {
             if (OP == 0) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(y), "v"(z));
@@ -254,11 +254,11 @@ double run(const char *name, int blocks, int per_iter) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u);
+    hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u, ITERS);
     (void)hipDeviceSynchronize();
     (void)hipEventRecord(a);
     const int reps = 5;
-    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u + r);
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u + r, ITERS);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float ms;
@@ -271,8 +271,59 @@ double run(const char *name, int blocks, int per_iter) {
     return rate;
 }
 
+/* round 5: the issue rate by waves per SIMD.  One generation of `wps` 256-thread blocks per CU (4 waves: one per SIMD),
+ * each wave running `iters` iterations of the pattern, best of 3 launches after a warm-up; the rate is per SIMD against
+ * its full-rate peak (2 cycles per wave64 instruction at 2.4 GHz), so 100 % = one full-rate instruction every 2 cycles */
+template <int OP>
+void run_occ(const char *name, int per_iter, int iters) {
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    unsigned *d;
+    (void)hipMalloc(&d, 4);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(k<OP>, dim3(ncu * 8), dim3(256), 0, 0, d, 1u, iters);
+    (void)hipDeviceSynchronize();
+    printf("%-22s", name);
+    for (int wps : {1, 2, 3, 4, 6, 8}) {
+        const int blocks = ncu * wps;
+        float best = 1e30f;
+        for (int r = 0; r < 3; r++) {
+            (void)hipEventRecord(a);
+            hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, d, 2u + r, iters);
+            (void)hipEventRecord(b);
+            (void)hipEventSynchronize(b);
+            float ms;
+            (void)hipEventElapsedTime(&ms, a, b);
+            best = ms < best ? ms : best;
+        }
+        const double lane_instr = (double)blocks * 256.0 * iters * CHAINS * per_iter;
+        const double rate = lane_instr / (best / 1e3);
+        /* cycles per wave-instruction on a SIMD: (SIMD-cycles) / (wave-instructions per SIMD) */
+        const double cyc = best / 1e3 * 2.4e9 / ((double)wps * iters * CHAINS * per_iter);
+        printf("  w%d %5.1f%% %4.2fc", wps, 100.0 * rate / 78.6432e12, cyc);
+    }
+    printf("\n");
+    (void)hipFree(d);
+}
+
 int main(int argc, char **argv) {
     const int blocks = 32768;
+    if (argc > 1 && argv[1][0] == 'o') {   /* "occ": issue rate by waves per SIMD */
+        const int it = 8192;
+        run_occ<3>("xor (F)", 1, it);
+        run_occ<65>("bitop3|xor indep (F)", 1, it);
+        run_occ<68>("bitop3 16 chains (F)", 2, it);
+        run_occ<2>("alignbit (H)", 1, it);
+        run_occ<0>("add3 (H)", 1, it);
+        run_occ<74>("alignbit|bitop3 alt", 1, it);
+        run_occ<70>("HHFF", 1, it);
+        run_occ<73>("7F 1H", 1, it);
+        run_occ<80>("odf mix (21)", 21, it / 8);
+        run_occ<82>("odf mix (21) il", 21, it / 8);
+        return 0;
+    }
     if (argc > 1) {   /* "mix": the KDF instruction mix against the additive slot model (78.64 T x 8 / 14.4) */
         run<53>("sha1 mix x8", blocks, 8);
         run<54>("sha1 mix x4 il", blocks, 4);
