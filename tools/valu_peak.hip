@@ -210,6 +210,11 @@ __global__ void __launch_bounds__(256) k(unsigned *out, unsigned seed, int iters
                 asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(x[c]) : "v"(y), "v"(z));
                 asm("v_alignbit_b32 %0, %0, %0, 2" : "+v"(x[c]));
             }
+            if (OP == 83) { /* round 5: the 21-instruction ODF pattern on two chains in instruction-level lockstep (A, B, A, B,
+                               ...): every instruction is followed by the same one on the other chain, independent of it */
+                if ((c & 1) == 0)
+                    asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_alignbit_b32 %1, %1, %1, 27\n\tv_bitop3_b32 %0, %0, %2, %3 bitop3:0xca\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0xca\n\tv_add3_u32 %0, %0, %2, %3\n\tv_add3_u32 %1, %1, %2, %3\n\tv_alignbit_b32 %0, %0, %0, 2\n\tv_alignbit_b32 %1, %1, %1, 2\n\tv_add3_u32 %0, %0, %3, %2\n\tv_add3_u32 %1, %1, %3, %2\n\tv_bitop3_b32 %0, %0, %2, %3 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0x96\n\tv_alignbit_b32 %0, %0, %0, 31\n\tv_alignbit_b32 %1, %1, %1, 31\n\tv_xor_b32 %0, %0, %2\n\tv_xor_b32 %1, %1, %2\n\tv_add3_u32 %0, %0, %2, %3\n\tv_add3_u32 %1, %1, %2, %3\n\tv_alignbit_b32 %0, %0, %0, 5\n\tv_alignbit_b32 %1, %1, %1, 5\n\tv_bitop3_b32 %0, %0, %2, %3 bitop3:0xe8\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0xe8\n\tv_add3_u32 %0, %0, %3, %2\n\tv_add3_u32 %1, %1, %3, %2\n\tv_alignbit_b32 %0, %0, %0, 30\n\tv_alignbit_b32 %1, %1, %1, 30\n\tv_add_u32 %0, %0, %2\n\tv_add_u32 %1, %1, %2\n\tv_alignbit_b32 %0, %0, %0, 1\n\tv_alignbit_b32 %1, %1, %1, 1\n\tv_bitop3_b32 %0, %0, %2, %3 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0x96\n\tv_add3_u32 %0, %0, %2, %3\n\tv_add3_u32 %1, %1, %2, %3\n\tv_alignbit_b32 %0, %0, %0, 27\n\tv_alignbit_b32 %1, %1, %1, 27\n\tv_xor_b32 %0, %0, %3\n\tv_xor_b32 %1, %1, %3\n\tv_bitop3_b32 %0, %0, %2, %3 bitop3:0xca\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0xca\n\tv_alignbit_b32 %0, %0, %0, 2\n\tv_alignbit_b32 %1, %1, %1, 2" : "+v"(x[c]), "+v"(x[c + 1]) : "v"(y), "v"(z));
+            }
             if (OP == 4) {
                 unsigned long long v = ((unsigned long long)x[c] << 32) | y;
                 asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(v) : "v"(((unsigned long long)z << 32) | z));
@@ -322,6 +327,7 @@ int main(int argc, char **argv) {
         run_occ<73>("7F 1H", 1, it);
         run_occ<80>("odf mix (21)", 21, it / 8);
         run_occ<82>("odf mix (21) il", 21, it / 8);
+        run_occ<83>("odf mix (21) lockstep2", 21, it / 8);
         return 0;
     }
     if (argc > 1) {   /* "mix": the KDF instruction mix against the additive slot model (78.64 T x 8 / 14.4) */
@@ -348,6 +354,7 @@ int main(int argc, char **argv) {
         run<80>("odf mix (21, add3)", blocks, 21);
         run<81>("odf mix (26, add3 as 2 add)", blocks, 26);
         run<82>("odf mix (21) chains interleaved", blocks, 21);
+        run<83>("odf mix (21) 2-chain lockstep", blocks, 21);
         printf("per 21-instruction unit of work: cycles = 21 x 157.29 T / rate(80) vs 26 x 157.29 T / rate(81)\n");
         run<2>("v_alignbit_b32", blocks, 1);
         run<0>("v_add3_u32", blocks, 1);
