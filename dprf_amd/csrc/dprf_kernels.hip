@@ -113,7 +113,9 @@ DEVI void report_hit(dprf_results *R, unsigned long long idx, uint32_t cap, uint
 }
 
 /* BE message words of `len` candidate bytes (LE-packed) placed after `pre` bytes already in m[],
- * pre a multiple of 4 and <= 16, with the 0x80 terminator.  Static indices only. */
+ * pre a multiple of 4 and <= 16, with the 0x80 terminator.  Static indices only.  A candidate that fills its whole
+ * 64-byte slot (Office: 32 UTF-16 units; ODF: 64 bytes) has its terminator in the word after the slot (round 5: until
+ * then it was dropped, and such a password was never found). */
 template <int PREW>
 DEVI void be_append(uint32_t m[32], const cand &c) {
 #pragma unroll
@@ -121,6 +123,7 @@ DEVI void be_append(uint32_t m[32], const cand &c) {
         m[PREW + j] = bswap32((c.w[j] & le_keep_mask(j, c.len)) | le_pad80(j, c.len));
 #pragma unroll
     for (int j = PREW + DPRF_SLOT_WORDS; j < 32; j++) m[j] = 0;
+    m[PREW + DPRF_SLOT_WORDS] = c.len == 4u * DPRF_SLOT_WORDS ? 0x80000000u : 0u;
 }
 
 /* SHA-1 / SHA-256 of a <= 119-byte message held in m[32] (BE, already terminated with 0x80):

@@ -122,3 +122,36 @@ def test_range_mode_at_the_length_limits(oracle, fmt, kind, kw, two_way):
                     want, nwant = octx.search_range(cs, n, s2, c2, nthreads=16)
                     got, ngot, _ = ctx.search_range(cs, n, s2, c2)
                     assert got == want and ngot == nwant and idx in want, (fmt, pw, got[:4], want[:4])
+
+
+# list mode: a password whose converted form fills the 64-byte slot exactly (Office 32 UTF-16 units, the rest 64
+# bytes), with its 63- and 65-byte neighbours (65: the long sub-list) -- round 5 found the slot-filling case lost
+# its SHA terminator in the Office and ODF kernels
+SLOT_FORMATS = FORMATS + [("pdf_r5", "pdf", {"R": 5, "length": 256}, 0)]
+
+
+def _slot_password(fmt):
+    if fmt == "office":
+        return "Sl0tFi11ing-" + "x" * 19 + "é"            # 32 UTF-16 units = 64 bytes
+    return "slot-filling:" + "0123456789abcdef" * 3 + "abc"     # 64 bytes
+
+
+def test_slot_passwords_fill_the_slot():
+    assert len(_slot_password("office").encode("utf-16-le")) == 64
+    assert len(_slot_password("odt").encode()) == 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,kind,kw,two_way", SLOT_FORMATS, ids=[f[0] for f in SLOT_FORMATS])
+def test_list_candidates_that_fill_the_slot(oracle, fmt, kind, kw, two_way):
+    from dprf_amd import _lib
+    pw = _slot_password(fmt)
+    words = [pw[:-1], pw, pw + "z", pw[:-1] + "q", "z" + pw[1:], pw[:-1] + "q" + "z"]
+    with tempfile.TemporaryDirectory() as t:
+        stream = _stream(t, kind, kw, pw)
+    want = [i for i, v in enumerate(oracle.Ctx(stream).verify_list(words)) if v == 1]
+    assert 1 in want, fmt
+    for devs in ([0], [0, 0]):
+        with _lib.Context(_fields(stream), devices=devs) as ctx:
+            hits, nh, st = ctx.verify_list(words)
+            assert hits == want and st["candidates"] == len(words), (fmt, devs, hits, want)
