@@ -1,0 +1,85 @@
+"""Planted passwords at the edges of the candidate domain (round 5).  The random-candidate and verdict-table tests
+compare verdicts, but most of their edge-case candidates are not any document's password, so a wrong hash of such a
+candidate still yields the right verdict (0).  That is how the slot-edge terminator bug stayed hidden until
+tests/test_range_limits.py planted a slot-filling password.  Here each edge case IS the document's password
+(tests/docgen.py writes the documents): the empty password for ODF and every PDF revision; Office passwords outside
+the BMP (UTF-16 surrogate pairs), accented and CJK ones, and ones whose UTF-16 form fills the 64-byte slot or just
+overflows it into the long sub-list; raw UTF-8 bytes for ODF and PDF.  The GPU verdicts must equal the oracle's (the
+CPU restatement of the reference verifiers) on one and two device lanes, and the password must be among the hits."""
+import contextlib
+import io
+import os
+import tempfile
+
+import pytest
+
+# (case id, writer kind, writer kwargs, planted password, other candidates of the list)
+CASES = [
+    ("odt-empty", "odt", {}, "", ["a", " ", "0"]),
+    ("pdf-r2-empty", "pdf", {"R": 2, "length": 40}, "", ["a", " "]),
+    ("pdf-r3-empty", "pdf", {"R": 3, "length": 128}, "", ["a", " "]),
+    ("pdf-r4-empty", "pdf", {"R": 4, "length": 128}, "", ["a", " "]),
+    ("pdf-r5-empty", "pdf", {"R": 5, "length": 256}, "", ["a", " "]),
+    ("pdf-r6-empty", "pdf", {"R": 6, "length": 256}, "", ["a", " "]),
+    ("office-emoji", "docx", {}, "\U0001F600ok", ["ok", "\U0001F601ok", "\U0001F600o"]),
+    ("office-accents", "docx", {}, "été", ["ete", "étè", "été "]),
+    ("office-cjk", "docx", {}, "日本語x", ["日本語", "日本x"]),
+    ("office-slot-surrogate", "docx", {}, "a" * 30 + "\U0001F600", ["a" * 30 + "\U0001F601", "a" * 31]),
+    ("office-long-surrogate", "docx", {}, "a" * 31 + "\U0001F600", ["a" * 31 + "\U0001F601", "a" * 32]),
+    ("odt-utf8", "odt", {}, "pässwörd", ["passwort", "pässwört"]),
+    ("pdf-r4-utf8", "pdf", {"R": 4, "length": 128}, "pässwörd", ["passwort", "pässwört"]),
+    ("pdf-r6-utf8", "pdf", {"R": 6, "length": 256}, "über-ß", ["uber-ss", "über-s"]),
+]
+
+
+def _stream(t, kind, kw, pw):
+    import docgen
+    from dprf_amd.parsers import odt2hashes, office2john, pdf2john
+    if kind == "docx":
+        path = os.path.join(t, "d.docx")
+        docgen.write_docx(path, pw, 0xED6)
+        return office2john.get_hash(path)
+    if kind == "odt":
+        path = os.path.join(t, "d.odt")
+        docgen.write_odt(path, pw, 0xED6)
+        return odt2hashes.get_hashes(path, False)
+    path = os.path.join(t, "d.pdf")
+    docgen.write_pdf(path, pw, 0xED6, **kw)
+    return pdf2john.get_hash(path)
+
+
+def _fields(stream):
+    from dprf_amd.brute_force import parse_verification_data
+    with contextlib.redirect_stdout(io.StringIO()):
+        return parse_verification_data(stream)
+
+
+def test_cases_hit_the_edges():
+    utf16 = {c[0]: len(c[3].encode("utf-16-le")) for c in CASES if c[1] == "docx"}
+    assert utf16["office-slot-surrogate"] == 64 and utf16["office-long-surrogate"] == 66
+    assert sum(1 for c in CASES if c[3] == "") == 6
+
+
+@pytest.mark.parametrize("name,kind,kw,pw,others", CASES, ids=[c[0] for c in CASES])
+def test_planted_edge_documents_verify_on_the_oracle(oracle, name, kind, kw, pw, others):
+    with tempfile.TemporaryDirectory() as t:
+        octx = oracle.Ctx(_stream(t, kind, kw, pw))
+    assert octx.verify(pw.encode()) == 1, name
+    assert octx.verify_list([o for o in others]) == [0] * len(others), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kind,kw,pw,others", CASES, ids=[c[0] for c in CASES])
+def test_gpu_finds_planted_edge_passwords(oracle, name, kind, kw, pw, others):
+    from dprf_amd import _lib
+    words = others[:1] + [pw] + others[1:]
+    with tempfile.TemporaryDirectory() as t:
+        stream = _stream(t, kind, kw, pw)
+    want = [i for i, v in enumerate(oracle.Ctx(stream).verify_list(words)) if v == 1]
+    assert 1 in want, name
+    for devs in ([0], [0, 0]):
+        with _lib.Context(_fields(stream), devices=devs) as ctx:
+            hits, nh, st = ctx.verify_list(words)
+            assert hits == want and st["candidates"] == len(words), (name, devs, hits, want)
+            fh, _, _ = ctx.verify_list(words, stop_on_first=True, cap=1)
+            assert fh == want[:1], (name, devs)
