@@ -155,3 +155,25 @@ def test_list_candidates_that_fill_the_slot(oracle, fmt, kind, kw, two_way):
         with _lib.Context(_fields(stream), devices=devs) as ctx:
             hits, nh, st = ctx.verify_list(words)
             assert hits == want and st["candidates"] == len(words), (fmt, devs, hits, want)
+
+
+# windows that cross 2^32: the library's launches carry a 64-bit start and 32-bit offsets within a launch, and its
+# chunking cuts calls at launch sizes; a planted password just below and just above 2^32
+CROSS = [("pdf_r5", "pdf", {"R": 5, "length": 256}), ("pdf_r4", "pdf", {"R": 4, "length": 128}),
+         ("odt", "odt", {})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,kind,kw", CROSS, ids=[c[0] for c in CROSS])
+def test_windows_across_2_32(oracle, fmt, kind, kw):
+    from dprf_amd import _lib
+    n = 7
+    for idx in (2 ** 32 - 1, 2 ** 32):
+        pw = word(idx, ALNUM, n)
+        with tempfile.TemporaryDirectory() as t:
+            stream = _stream(t, kind, kw, pw)
+        assert oracle.Ctx(stream).verify(pw.encode()) == 1
+        with _lib.Context(_fields(stream), devices=[0, 0]) as ctx:
+            for start, count in ((2 ** 32 - 1500, 3000), (idx, 1), (2 ** 32 - 2 ** 21, 2 ** 22)):
+                hits, _, st = ctx.search_range(ALNUM, n, start, count)
+                assert st["candidates"] == count and hits == [idx], (fmt, idx, start, count, hits)
