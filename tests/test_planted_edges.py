@@ -4,8 +4,9 @@ candidate still yields the right verdict (0).  That is how the slot-edge termina
 tests/test_range_limits.py planted a slot-filling password.  Here each edge case IS the document's password
 (tests/docgen.py writes the documents): the empty password for ODF and every PDF revision; Office passwords outside
 the BMP (UTF-16 surrogate pairs), accented and CJK ones, and ones whose UTF-16 form fills the 64-byte slot or just
-overflows it into the long sub-list; raw UTF-8 bytes for ODF and PDF.  The GPU verdicts must equal the oracle's (the
-CPU restatement of the reference verifiers) on one and two device lanes, and the password must be among the hits."""
+overflows it into the long sub-list; raw UTF-8 bytes for ODF and PDF; the first hash's one-to-two block edges.  The
+GPU verdicts must equal the oracle's (the CPU restatement of the reference verifiers) on one and two device lanes,
+and the password must be among the hits."""
 import contextlib
 import io
 import os
@@ -29,6 +30,14 @@ CASES = [
     ("odt-utf8", "odt", {}, "pässwörd", ["passwort", "pässwört"]),
     ("pdf-r4-utf8", "pdf", {"R": 4, "length": 128}, "pässwörd", ["passwort", "pässwört"]),
     ("pdf-r6-utf8", "pdf", {"R": 6, "length": 256}, "über-ß", ["uber-ss", "über-s"]),
+    # the one-to-two block edges of the first hash in list mode: ODF SHA-256(pw) at 55 / 56 bytes, R5 / R6
+    # SHA-256(pw || salt8) at 47 / 48 bytes of password
+    ("odt-55", "odt", {}, "e" * 55, ["e" * 54, "e" * 56]),
+    ("odt-56", "odt", {}, "f" * 56, ["f" * 55, "f" * 57]),
+    ("pdf-r5-47", "pdf", {"R": 5, "length": 256}, "g" * 47, ["g" * 46, "g" * 48]),
+    ("pdf-r5-48", "pdf", {"R": 5, "length": 256}, "h" * 48, ["h" * 47, "h" * 49]),
+    ("pdf-r6-47", "pdf", {"R": 6, "length": 256}, "i" * 47, ["i" * 46, "i" * 48]),
+    ("pdf-r6-48", "pdf", {"R": 6, "length": 256}, "j" * 48, ["j" * 47, "j" * 49]),
 ]
 
 

@@ -1,7 +1,7 @@
 """Range mode at the length limits, every format (round 5).  brute_force.py enumerates -pr N over lengths 1..N
 (:199-219); the library spells a keyspace index on the device for any length up to DPRF_MAX_RANGE_LEN = 32 bytes.
-Each case plants a password of length 1, 4, 5, 16, 17, 31 or 32 (every candidate-word boundary, the SHA-256 / SHA-1
-one-block edges after the format's prefix, PDF R2-R4's 32-byte truncation point, Office's 64-byte UTF-16 slot) in a
+Each case plants a password of length 1, 4, 5, 16, 17, 19, 20, 31 or 32 (every candidate-word boundary, Office's
+one-to-two SHA-1 block edge after its 16-byte salt, PDF R2-R4's 32-byte truncation point, Office's 64-byte UTF-16 slot) in a
 self-generated document (tests/docgen.py) and searches a window around its keyspace index over a two-character
 charset (so 2^32 indices reach length 32), plus a 10-character alphanumeric one past 2^32.  The planted index must be
 the lowest hit, every hit must verify on the oracle (the CPU restatement of the reference verifiers), and over a
@@ -32,6 +32,8 @@ PASSWORDS = [
     (AB, "babab"),
     (AB, "ab" * 8),
     (AB, "ba" * 8 + "b"),
+    (AB, "abbaabbaabbaabbaabb"),    # 19: Office's salt + UTF-16 = 54 bytes, one SHA-1 block
+    (AB, "baabbaabbaabbaabbaab"),   # 20: 56 bytes, two blocks
     (AB, "a" + "ba" * 15),
     (AB, "b" * 31 + "a"),
     (ALNUM, "Zq7pLm0a9X"),
@@ -85,7 +87,7 @@ def _window(pw, cs, size=WINDOW):
 
 def test_cases_cover_the_length_limits():
     lens = {len(pw) for _, pw in PASSWORDS}
-    assert {1, 4, 5, 16, 17, 31, 32} <= lens
+    assert {1, 4, 5, 16, 17, 19, 20, 31, 32} <= lens
     idx, start, count = _window(*reversed(PASSWORDS[-1]))
     assert start > 2 ** 32 and start <= idx < start + count
 
