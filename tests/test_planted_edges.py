@@ -92,3 +92,58 @@ def test_gpu_finds_planted_edge_passwords(oracle, name, kind, kw, pw, others):
             assert hits == want and st["candidates"] == len(words), (name, devs, hits, want)
             fh, _, _ = ctx.verify_list(words, stop_on_first=True, cap=1)
             assert fh == want[:1], (name, devs)
+
+
+# ODF encrypted-entry lengths: the check hashes min(enc_len, 1024) decrypted bytes (odt_password_verifier.c:104-111),
+# so every length below 1024 -- one SHA-256 block or several, the bit length in the same block as the last data or
+# in one of its own -- takes a different path through the check kernel, and enc_len 16 is the 2-byte check
+# (:98-101).  Writers only produce entries of > 1024 bytes for the standard stream, so these $odt$ streams are built
+# directly: a known password's key, a random plaintext (03 00 ... for the 2-byte check), and the checksum the
+# reference computes over its decrypted prefix.
+ODT_LENGTHS = [16, 32, 48, 64, 80, 112, 496, 1008, 1024, 1040, 2048]
+
+
+def _odt_stream(pw, n, seed):
+    """no field may start with a 00 byte: the reference's str_to_uchar decodes such a hex field short (the
+    library flags that as DPRF_FLAG_REF_NONDETERMINISTIC), as tests/docgen.py avoids for its documents too"""
+    import hashlib
+    import random
+    import docgen
+    rng = random.Random(seed)
+    while True:
+        salt, iv = bytes(rng.getrandbits(8) for _ in range(16)), bytes(rng.getrandbits(8) for _ in range(16))
+        plain = bytearray(rng.getrandbits(8) for _ in range(n))
+        if n == 16:
+            plain[0:2] = b"\x03\x00"
+        enc = docgen._aes_cbc(docgen.odt_key(pw, salt), iv, bytes(plain))
+        checksum = hashlib.sha256(bytes(plain[:min(n, 1024)])).digest()
+        if all(f[0] for f in (salt, iv, enc, checksum)):
+            return "len%d.odt:$odt$*1.2*%s*%s*%s*%s*%d" % (n, checksum.hex(), iv.hex(), salt.hex(), enc.hex(), n)
+
+
+@pytest.mark.parametrize("n", ODT_LENGTHS)
+def test_odt_entry_lengths_on_the_oracle(oracle, n):
+    octx = oracle.Ctx(_odt_stream("Lk9#q", n, n))
+    assert octx.verify(b"Lk9#q") == 1
+    assert octx.verify(b"Lk9#r") == 0 or n == 16          # the 2-byte check lets 2^-16 through
+
+
+@pytest.mark.gpu
+def test_gpu_odt_entry_lengths():
+    import pyoracle
+    from dprf_amd import _lib
+    words = ["Lk9#p", "Lk9#q", "Lk9#r", "Lk9#", "Lk9#qq"]
+    for n in ODT_LENGTHS:
+        stream = _odt_stream("Lk9#q", n, n)
+        want = [i for i, v in enumerate(pyoracle.Ctx(stream).verify_list(words)) if v == 1]
+        assert 1 in want, n
+        with _lib.Context(_fields(stream), device=0) as ctx:
+            hits, _, _ = ctx.verify_list(words)
+            assert hits == want, (n, hits, want)
+            # range mode over the 5-character space around the password too
+            cs = "#9kLpqr"
+            idx = sum(cs.index(ch) * len(cs) ** (4 - k) for k, ch in enumerate("Lk9#q"))
+            rh, _, _ = ctx.search_range(cs, 5, max(0, idx - 300), 600)
+            octx = pyoracle.Ctx(stream)
+            want_r, _ = octx.search_range(cs, 5, max(0, idx - 300), 600, nthreads=16)
+            assert rh == want_r and idx in rh, (n, rh[:4], want_r[:4])
