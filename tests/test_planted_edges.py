@@ -147,3 +147,107 @@ def test_gpu_odt_entry_lengths():
             octx = pyoracle.Ctx(stream)
             want_r, _ = octx.search_range(cs, 5, max(0, idx - 300), 600, nthreads=16)
             assert rh == want_r and idx in rh, (n, rh[:4], want_r[:4])
+
+
+# PDF R2-R4 document IDs of other lengths: the first MD5 hashes pw32 || O || P || ID [|| FFFFFFFF] (pdf...c:136-139,
+# :352-402), so the ID length moves the message across the 55/64 and 119/128-byte block edges and the library's
+# document tail (dprf_pdf_params.tail) takes 2-4 blocks.  Writers use 16-byte IDs; these streams are built directly
+# with tests/docgen.py's algorithms (O, the key, U) for IDs of 1-100 bytes, metadata on and off.
+PDF_IDS = [(2, 1, True), (2, 40, True), (3, 16, True), (3, 48, True), (3, 52, True), (4, 23, True),
+           (4, 24, False), (4, 47, False), (4, 48, False), (4, 51, True), (4, 100, False), (3, 32, True)]
+
+
+def _pdf_stream(pw, R, idlen, meta, seed):
+    import hashlib
+    import random
+    import docgen
+    rng = random.Random(seed)
+    n = 5 if R == 2 else 16
+    P = -3904
+    while True:
+        ID = bytes(rng.getrandbits(8) for _ in range(idlen))
+        O_ = docgen._pdf_owner("owner", pw, R, n)
+        key = docgen._pdf_key(pw, O_, P, ID, R, n, meta)
+        if R == 2:
+            U = docgen.O.rc4(key, docgen.PDF_PAD)
+        else:
+            c = docgen.O.rc4(key, hashlib.md5(docgen.PDF_PAD + ID).digest())
+            for i in range(1, 20):
+                c = docgen.O.rc4(bytes(k ^ i for k in key), c)
+            U = c + bytes(rng.getrandbits(8) for _ in range(16))
+        if U[0] and O_[0] and ID[0]:
+            break
+    V = {2: 1, 3: 2, 4: 4}[R]
+    return "id%d.pdf:$pdf$*%d*%d*%d*%d*%d*%d*%s*%d*%s*%d*%s" % (idlen, V, R, 8 * n, P, 1 if meta else 0, idlen,
+                                                                  ID.hex(), len(U), U.hex(), len(O_), O_.hex())
+
+
+@pytest.mark.parametrize("R,idlen,meta", PDF_IDS)
+def test_pdf_id_lengths_on_the_oracle(oracle, R, idlen, meta):
+    octx = oracle.Ctx(_pdf_stream("Tq8$z", R, idlen, meta, idlen))
+    assert octx.verify(b"Tq8$z") == 1 and octx.verify(b"Tq8$y") == 0
+
+
+@pytest.mark.gpu
+def test_gpu_pdf_id_lengths():
+    import pyoracle
+    from dprf_amd import _lib
+    words = ["Tq8$y", "Tq8$z", "Tq8$", "Tq8$zz"]
+    cs = "$8Tqyz"
+    idx = sum(cs.index(ch) * len(cs) ** (4 - k) for k, ch in enumerate("Tq8$z"))
+    for R, idlen, meta in PDF_IDS:
+        stream = _pdf_stream("Tq8$z", R, idlen, meta, idlen)
+        octx = pyoracle.Ctx(stream)
+        want = [i for i, v in enumerate(octx.verify_list(words)) if v == 1]
+        assert want == [1], (R, idlen)
+        with _lib.Context(_fields(stream), devices=[0, 0]) as ctx:
+            hits, _, _ = ctx.verify_list(words)
+            assert hits == want, (R, idlen, meta, hits)
+            rh, _, _ = ctx.search_range(cs, 5, 0, len(cs) ** 5)
+            want_r, _ = octx.search_range(cs, 5, 0, len(cs) ** 5, nthreads=16)
+            assert rh == want_r and idx in rh, (R, idlen, meta, rh[:4], want_r[:4])
+
+
+# Office verifier-hash sizes: the reference checks byte hash_size of the decrypted verifier hash for zero before the
+# SHA-1 compare (msoffcrypto...c:168), a byte the check kernel picks at run time.  Writers use 20 (a padding byte);
+# these streams take 0-31, with a verifier whose SHA-1 has a zero at that byte when it lies inside the hash.
+OFFICE_HASH_SIZES = [0, 3, 7, 19, 20, 21, 27, 31]
+
+
+def _office_stream(pw, hs, seed):
+    import hashlib
+    import random
+    import docgen
+    rng = random.Random(seed)
+    salt = bytes([rng.getrandbits(8) | 1]) + bytes(rng.getrandbits(8) for _ in range(15))
+    key = docgen.office_key(pw, salt)
+    while True:
+        verifier = bytes(rng.getrandbits(8) for _ in range(16))
+        vh = hashlib.sha1(verifier).digest() + b"\0" * 12
+        ev, evh = docgen._aes_ecb(key, verifier), docgen._aes_ecb(key, vh)
+        if vh[hs] == 0 and ev[0] and evh[0]:
+            return "hs%d.docx:$office$*2007*%d*128*16*%s*%s*%s" % (hs, hs, salt.hex(), ev.hex(), evh.hex())
+
+
+@pytest.mark.parametrize("hs", OFFICE_HASH_SIZES)
+def test_office_hash_sizes_on_the_oracle(oracle, hs):
+    octx = oracle.Ctx(_office_stream("Ux7", hs, hs))
+    assert octx.verify("Ux7".encode()) == 1 and octx.verify(b"Ux8") == 0
+
+
+@pytest.mark.gpu
+def test_gpu_office_hash_sizes():
+    import pyoracle
+    from dprf_amd import _lib
+    words = ["Ux6", "Ux7", "Ux8", "Ux", "Ux77"]
+    for hs in OFFICE_HASH_SIZES:
+        stream = _office_stream("Ux7", hs, hs)
+        want = [i for i, v in enumerate(pyoracle.Ctx(stream).verify_list(words)) if v == 1]
+        assert want == [1], hs
+        with _lib.Context(_fields(stream), device=0) as ctx:
+            hits, _, _ = ctx.verify_list(words)
+            assert hits == want, (hs, hits)
+            cs = "678Ux"
+            idx = sum(cs.index(ch) * len(cs) ** (2 - k) for k, ch in enumerate("Ux7"))
+            rh, _, _ = ctx.search_range(cs, 3, 0, len(cs) ** 3)
+            assert rh == [idx], (hs, rh)
