@@ -74,6 +74,99 @@ __global__ void __launch_bounds__(64) k_time(const uint32_t *keys, uint32_t *sin
     sink[g] = d[0];
 }
 
+/* Timing mode 2 (round 5): the same RC4 work in the product's workgroup shape -- 128 threads, wave 0 the RC4 chain, wave 1
+ * resident but idle at the closing barrier (a waiting wave takes no issue slots) -- so the SIMDs and the LDS see the
+ * product's placement of 9 chains per CU without its key derivation */
+template <int NK, int R>
+__global__ void __launch_bounds__(128) k_time2(const uint32_t *keys, uint32_t *sink, int passes) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
+    if (threadIdx.x >= 64) {
+        __syncthreads();
+        return;
+    }
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)S);
+    const uint32_t lane = threadIdx.x;
+    const size_t g = (size_t)blockIdx.x * 64u + lane;
+    uint32_t k[4] = {keys[4 * (g & 4095)], keys[4 * (g & 4095) + 1], keys[4 * (g & 4095) + 2], keys[4 * (g & 4095) + 3]};
+    uint32_t kb[rc4_nkr<NK>::v];
+    rc4_kb_init<NK>(k, kb);
+    uint32_t d[4] = {0, 0, 0, 0};
+    for (int x = 0; x < passes; x++) {
+        const uint32_t dx = (uint32_t)x ^ (uint32_t)(x - 1);
+#pragma unroll
+        for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+        rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
+        if (R == 2) {
+            uint32_t jj = 0;
+            rc4_prga_span<1, 4>(S, lane << 2, d, jj);
+        } else {
+            rc4_prga<2>(S, lane << 2, d);
+        }
+    }
+    sink[g] = d[0];
+    __syncthreads();
+}
+
+template <int NK, int R>
+static void time_passes2(int passes) {
+    int ncu = 0;
+    CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    std::vector<uint32_t> keys(4096 * 4);
+    uint64_t st = 0x243F6A8885A308D3ull;
+    for (auto &w : keys) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; w = (uint32_t)st; }
+    uint32_t *dk, *ds;
+    CHECK(hipMalloc(&dk, keys.size() * 4));
+    CHECK(hipMalloc(&ds, (size_t)ncu * 10 * 64 * 4));
+    CHECK(hipMemcpy(dk, keys.data(), keys.size() * 4, hipMemcpyHostToDevice));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
+    for (int r = 0; r < 8; r++) hipLaunchKernelGGL((k_time2<NK, R>), dim3(ncu * 9), dim3(128), 0, 0, dk, ds, passes);
+    CHECK(hipDeviceSynchronize());
+    for (int wpc : {4, 8, 9}) {
+        const int blocks = ncu * wpc;
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; rep++) {
+            CHECK(hipEventRecord(a, 0));
+            hipLaunchKernelGGL((k_time2<NK, R>), dim3(blocks), dim3(128), 0, 0, dk, ds, passes);
+            CHECK(hipEventRecord(b, 0));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            best = ms < best ? ms : best;
+        }
+        const double pass_ns = best * 1e6 / passes;
+        const double rate = (double)blocks * 64 / ((R == 2 ? 1.0 : 20.0) * pass_ns * 1e-9);
+        printf("{\"mode\": \"128-thread workgroups, idle second wave\", \"r\": %d, \"nk\": %d, \"chains_per_cu\": %d, "
+               "\"passes\": %d, \"ms\": %.3f, \"pass_ns\": %.1f, \"cand_per_s\": %.4g}\n", R, NK, wpc, passes, best,
+               pass_ns, rate);
+    }
+    /* many generations, as the product runs: 30 workgroups' worth per resident slot, each of passes / 20 passes, so
+     * a SIMD that frees first takes the next workgroup (the single generation above waits for its busiest SIMD) */
+    {
+        const int gens = 30, wp = passes / 20 > 0 ? passes / 20 : 1;
+        const int blocks = ncu * 9 * gens;
+        uint32_t *dsb;
+        CHECK(hipMalloc(&dsb, (size_t)blocks * 64 * 4));
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; rep++) {
+            CHECK(hipEventRecord(a, 0));
+            hipLaunchKernelGGL((k_time2<NK, R>), dim3(blocks), dim3(128), 0, 0, dk, dsb, wp);
+            CHECK(hipEventRecord(b, 0));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            best = ms < best ? ms : best;
+        }
+        const double cand = (double)blocks * 64 * wp / (R == 2 ? 1.0 : 20.0);
+        printf("{\"mode\": \"128-thread workgroups, idle second wave, %d generations of 9 per CU\", \"r\": %d, "
+               "\"nk\": %d, \"passes_per_workgroup\": %d, \"ms\": %.3f, \"pass_ns_per_chain\": %.1f, "
+               "\"cand_per_s\": %.4g}\n", gens, R, NK, wp, best, best * 1e6 * ncu * 9 / ((double)blocks * wp),
+               cand / (best * 1e-3));
+        CHECK(hipFree(dsb));
+    }
+    CHECK(hipFree(dk)); CHECK(hipFree(ds));
+}
+
 template <int NK, int R>
 static void time_passes(int passes) {
     int ncu = 0;
@@ -182,6 +275,13 @@ static int run(int blocks, int passes) {
 }
 
 int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "time2")) {         /* rc4_ksa_probe time2 [passes] */
+        const int passes = argc > 2 ? atoi(argv[2]) : 4000;
+        if (passes < 1 || passes > 100000) { printf("bad args\n"); return 2; }
+        time_passes2<16, 3>(passes);
+        time_passes2<5, 2>(passes);
+        return 0;
+    }
     if (argc > 1 && !strcmp(argv[1], "time")) {          /* rc4_ksa_probe time [passes] */
         const int passes = argc > 2 ? atoi(argv[2]) : 4000;
         if (passes < 1 || passes > 100000) { printf("bad args\n"); return 2; }
