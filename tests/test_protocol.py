@@ -393,3 +393,29 @@ def test_config5_office_testdoc_first_mi_of_pr8_no_hit(streams):
         assert st == pos
         pos += c
     assert pos == n
+
+
+@pytest.mark.gpu
+def test_gpu_client_finds_passwords_at_payload_and_length_edges(tmp_path):
+    """Planted passwords at the edges of the server's order (server.py:189-199): the last and first candidate of a
+    payload, the last candidate of one length and the first of the next, and the keyspace's very last candidate --
+    each in a fresh PDF R4 document (tests/docgen.py), found by the real GPU client through the server."""
+    import docgen
+    from dprf_amd.parsers import pdf2john
+    ks = pl.Keyspace(pl.LOWERCASE, 3)
+    ps = 1000
+    for g in (5 * ps - 1, 5 * ps, ks.sizes[0] + ks.sizes[1] - 1, ks.sizes[0] + ks.sizes[1], ks.total - 1):
+        L = next(L for L, s, c in ks.segments(g, 1))
+        start = sum(ks.sizes[:L - 1])
+        pw = ks.password(L, g - start)
+        assert ks.global_index(pw) == g
+        path = str(tmp_path / ("edge%d.pdf" % g))
+        docgen.write_pdf(path, pw, g, R=4, length=128)
+        srv = sv.Server(pdf2john.get_hash(path), password_range=3, payload_size=ps, heartbeat_port=_free_port(),
+                        quiet=True)
+        th, out = _run_server(srv)
+        ver = cl.GpuVerifier([0])
+        rc, found = cl.connect_to_server("127.0.0.1", srv.address[1], "gpu", ver, quiet=True)
+        ver.close()
+        th.join(10)
+        assert (rc, found) == (0, pw) and out["pw"] == pw, (g, pw, rc, found)
