@@ -196,7 +196,13 @@ class Context:
 
     def search_range(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
         """Verify keyspace indices [start, start+count) of charset^pwlen (itertools.product order).
-        Returns (sorted hit indices (at most cap), total hits, stats dict)."""
+        Returns (sorted hit indices (at most cap), total hits, stats dict).  The library's symbols are bytes: a str
+        charset must be ASCII (a character of several UTF-8 bytes would enumerate as several symbols -- a different
+        keyspace; brute_force.search_round spells such windows on the host instead), a bytes charset is taken as
+        byte symbols (include/dprf.h dprf_search_range)."""
+        if isinstance(charset, str) and any(ord(ch) >= 0x80 for ch in charset):
+            raise DprfError(E_CHARSET, "search_range enumerates byte symbols: charset %r has multi-byte characters "
+                                       "(brute_force.search_round verifies such windows in list mode)" % charset)
         cs = _to_bytes(charset)
         hits = (ctypes.c_uint64 * max(1, cap))()
         nh = ctypes.c_int64()

@@ -19,8 +19,8 @@ candidates go to libdprf.so in batches, one candidate per GPU lane.  Differences
 * a verifier error is raised as :class:`dprf_amd._lib.DprfError`, never reported as found (the reference
   counts any non-zero exit as a hit, :140; Appendix B.6).
 * optional keyword arguments ``charset`` (default lowercase a-z, Python 2 ``string.lowercase`` in the C
-  locale), ``devices`` (default: every visible gfx950 GPU) and ``checkpoint`` (a resumable cursor file
-  for range mode, :class:`Checkpoint`).
+  locale; distinct characters, any of them non-ASCII too -- :func:`check_charset`), ``devices`` (default:
+  every visible gfx950 GPU) and ``checkpoint`` (a resumable cursor file for range mode, :class:`Checkpoint`).
 
 The reference's four worker processes on one queue (:70-73, :92-95) are inside libdprf.so: one context
 spans the devices, and every search call fans out over them (one worker thread + HIP stream per GPU on a
@@ -163,12 +163,55 @@ def progress(t0, tried, remaining):
     sys.stdout.flush()
 
 
+def check_charset(charset):
+    """The range-mode alphabet: a non-empty str of distinct characters without NUL (NUL cannot reach the reference's
+    verifier through argv).  Returns True when every character is one byte (ASCII) -- the library enumerates such a
+    charset on the device (dprf_search_range) -- and False when some character takes more UTF-8 bytes: the library's
+    range symbols are bytes, so such a window is spelled on the host by characters (payload.spell_utf8) and verified in
+    list mode (dprf_verify_list), the keyspace staying charset^N over characters as itertools.product has it
+    (brute_force.py:199-219).  Raises DprfError(E_CHARSET) otherwise."""
+    if not isinstance(charset, str):
+        raise _lib.DprfError(_lib.E_CHARSET, "charset must be a str (got %s)" % type(charset).__name__)
+    if not charset:
+        raise _lib.DprfError(_lib.E_CHARSET, "empty charset")
+    if "\0" in charset:
+        raise _lib.DprfError(_lib.E_CHARSET, "charset contains NUL (the reference passes candidates via argv)")
+    if len(set(charset)) != len(charset):
+        dup = next(c for c in charset if charset.count(c) > 1)
+        raise _lib.DprfError(_lib.E_CHARSET, "charset repeats %r (itertools.product would verify candidates twice)"
+                             % dup)
+    try:
+        charset.encode("utf-8")
+    except UnicodeEncodeError as e:   # lone surrogates
+        raise _lib.DprfError(_lib.E_CHARSET, "charset is not encodable as UTF-8: %s" % e)
+    return all(ord(c) < 0x80 for c in charset)
+
+
+WIDE_ROUND = 1 << 21   # candidates per library call of a host-spelled (non-ASCII charset) round
+
+
 def search_round(ctx, charset, pwlen, start, count, stop_on_first=True):
     """One round of range mode on every device of ctx: (lowest hit index or None, stats).  The same call
     bench.py times per rank (there with stop_on_first=False: a throughput step verifies its whole batch
-    even when a false positive of ODF -e's 2-byte check turns up in it)."""
-    hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
-    return (hits[0] if hits else None), st
+    even when a false positive of ODF -e's 2-byte check turns up in it).  A charset with multi-byte characters
+    (check_charset False) is spelled on the host and verified as a list, in calls of WIDE_ROUND candidates."""
+    if check_charset(charset):
+        hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
+        return (hits[0] if hits else None), st
+    from .payload import spell_utf8
+    total = {"candidates": 0, "wall_ms": 0.0}
+    found = None
+    for s in range(start, start + count, WIDE_ROUND):
+        n = min(WIDE_ROUND, start + count - s)
+        blob, offs = spell_utf8(charset, pwlen, s, n)
+        hits, _, st = ctx.verify_blob(blob, offs, stop_on_first=stop_on_first, cap=1)
+        total["candidates"] += st["candidates"]
+        total["wall_ms"] += st["wall_ms"]
+        if hits and found is None:
+            found = s + hits[0]
+            if stop_on_first:
+                break
+    return found, total
 
 
 def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, devices=None, checkpoint=None):
@@ -177,7 +220,8 @@ def init_rangebased_brute_force(input_data, password_range, charset=LOWERCASE, d
     Rounds of consecutive indices, each one library call over all devices with stop_on_first: a round
     returns its lowest hit, every index below a round's end has been verified once it returns, so the first
     round with a hit holds the lowest hit overall.  checkpoint: path of a resumable cursor file
-    (:class:`Checkpoint`)."""
+    (:class:`Checkpoint`).  charset: see check_charset (raises before any device work)."""
+    check_charset(charset)
     cp = Checkpoint(checkpoint, input_data, charset, password_range)
     done, prior = cp.load()
     if prior is not None:

@@ -112,6 +112,30 @@ def segment_chars(charset, length, start, count, out=None):
     return out
 
 
+def spell_utf8(charset, length, start, count):
+    """(blob, offsets) of keyspace indices [start, start+count) of charset^length in itertools.product order, each
+    candidate the UTF-8 encoding of its characters: the dprf_verify_list form of a range window whose symbols are not
+    all single bytes (range mode over a non-ASCII charset, brute_force.init_rangebased_brute_force).  A character is
+    one symbol whatever its UTF-8 length, as in ``itertools.product(charset, repeat=length)``."""
+    syms = [c.encode("utf-8") for c in charset]
+    n, width = len(syms), max(len(s) for s in syms)
+    table = np.zeros((n, width), dtype=np.uint8)
+    for k, s in enumerate(syms):
+        table[k, :len(s)] = np.frombuffer(s, dtype=np.uint8)
+    slen = np.array([len(s) for s in syms], dtype=np.int64)
+    idx = np.arange(count, dtype=np.uint64) + np.uint64(start)
+    digits = np.empty((count, length), dtype=np.int64)
+    for p in range(length - 1, -1, -1):
+        digits[:, p] = (idx % np.uint64(n)).astype(np.int64)
+        idx //= np.uint64(n)
+    lens = slen[digits]                                        # [count, length] bytes per character
+    keep = np.arange(width)[None, None, :] < lens[:, :, None]  # the used bytes of each padded character
+    blob = table[digits][keep].tobytes()
+    offs = np.zeros(count + 1, dtype=np.uint64)
+    np.cumsum(lens.sum(axis=1), out=offs[1:])
+    return blob, offs
+
+
 def build_message(stream, charset, segments):
     """The server's JSON payload for these segments, as bytes (same text json.dumps gives, key order
     data, passwords)."""

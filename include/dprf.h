@@ -48,7 +48,8 @@ extern "C" {
 #define DPRF_E_NODEVICE (-4)     /* no usable gfx950 device / bad device ordinal                  */
 #define DPRF_E_PWLEN (-5)        /* candidate too long: over DPRF_MAX_PW bytes (list mode; no argv string can carry
                                     it to the reference), or a range length over DPRF_MAX_PW_RANGE  */
-#define DPRF_E_CHARSET (-6)      /* charset invalid for this format (e.g. non-ASCII for Office)    */
+#define DPRF_E_CHARSET (-6)      /* range charset invalid: empty, NUL, a repeated byte, or a byte >= 0x80
+                                    for Office (its candidates are UTF-16LE of characters)           */
 
 #define DPRF_ALL_DEVICES (-1)    /* dprf_ctx_create device argument: every gfx950 device visible    */
 #define DPRF_MAX_DEVICES 64
@@ -148,7 +149,10 @@ int dprf_ctx_last_call_devices(const dprf_ctx *ctx, dprf_device_stats *out, int 
 
 /* ---- range mode: brute_force.py -pr N (init_rangebased_brute_force :60-79, _generate :199-219) ----
  * Verifies candidates [start, start+count) of charset^pwlen in itertools.product order (leftmost
- * character most significant).  Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total
+ * character most significant).  The symbols are the charset's BYTES, all distinct (a repeated byte would
+ * verify candidates twice: DPRF_E_CHARSET): for PDF and ODF a byte >= 0x80 is a raw candidate byte, as the
+ * reference's argv carries it; Office takes ASCII only.  A caller whose alphabet has multi-byte UTF-8
+ * characters spells the window itself and verifies it with dprf_verify_list (brute_force.search_round).  Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total
  * number of hits found (may exceed cap).  stats may be NULL.
  * Multi-device: the devices take contiguous chunks of the range from one shared cursor in increasing
  * order (chunks sized for ~0.1-1 s of device time at the rate measured on that device), so a fast device
