@@ -74,37 +74,6 @@ DEVI void sha1_compress(uint32_t st[5], uint32_t w[16]) {
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
 }
-/* Two independent compressions statement by statement in lockstep (round 5 A/B, OFFICE_KDF_PAIR: two candidates per
- * lane in the Office loop, see sha1_compress_pre2). */
-DEVI void sha1_compress2(uint32_t st[2][5], uint32_t w[2][16]) {
-    uint32_t a[2], b[2], c[2], d[2], e[2];
-#pragma unroll
-    for (int x = 0; x < 2; x++) { a[x] = st[x][0]; b[x] = st[x][1]; c[x] = st[x][2]; d[x] = st[x][3]; e[x] = st[x][4]; }
-#pragma unroll
-    for (int t = 0; t < 80; t++) {
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            uint32_t wt;
-            if (t < 16) {
-                wt = w[x][t];
-            } else {
-                wt = rol32(xor3(w[x][(t - 3) & 15], w[x][(t - 8) & 15], w[x][(t - 14) & 15]) ^ w[x][t & 15], 1);
-                w[x][t & 15] = wt;
-            }
-            uint32_t f, k;
-            if (t < 20)      { f = f_ch(b[x], c[x], d[x]);  k = 0x5A827999u; }
-            else if (t < 40) { f = xor3(b[x], c[x], d[x]);  k = 0x6ED9EBA1u; }
-            else if (t < 60) { f = f_maj(b[x], c[x], d[x]); k = 0x8F1BBCDCu; }
-            else             { f = xor3(b[x], c[x], d[x]);  k = 0xCA62C1D6u; }
-            const uint32_t tmp = rol32(a[x], 5) + f + e[x] + (k + wt);
-            e[x] = d[x]; d[x] = c[x]; c[x] = rol32(b[x], 30); b[x] = a[x]; a[x] = tmp;
-        }
-    }
-#pragma unroll
-    for (int x = 0; x < 2; x++) {
-        st[x][0] += a[x]; st[x][1] += b[x]; st[x][2] += c[x]; st[x][3] += d[x]; st[x][4] += e[x];
-    }
-}
 /* SHA-1 from a fixed starting state (PBKDF2's HMAC midstates: the same for all 1,023 iterations of a candidate).
  * sha1_pre computes, once per candidate, everything of rounds 0-4 that does not depend on the message: round 0's
  * whole sum but w0, round 1's f + e + k as ONE value (LLVM hoists f and e + k as two), and e + k of rounds 2-4.  They
@@ -154,50 +123,6 @@ DEVI void sha1_compress_pre(const uint32_t st[5], const sha1_pre_t &P, uint32_t 
         e = d; d = c; c = rol32(b, 30); b = a; a = tmp;
     }
     out[0] = st[0] + a; out[1] = st[1] + b; out[2] = st[2] + c; out[3] = st[3] + d; out[4] = st[4] + e;
-}
-/* Two independent compressions from the same starting state, statement by statement in lockstep (round 5 A/B,
- * ODT_KDF_PAIR): the two PBKDF2 output blocks of one candidate as two interleaved instruction streams, so no VALU
- * instruction depends on the one before it (tools/valu_peak.hip: the KDF's 21-instruction mix issues at 3.75 cycles
- * per wave-instruction with independent chains interleaved, 3.95 back to back). */
-DEVI void sha1_compress_pre2(const uint32_t st[5], const sha1_pre_t &P, uint32_t w[2][16], uint32_t out[2][5]) {
-    const uint32_t K = 0x5A827999u;
-    uint32_t a[2], b[2], c[2], d[2], e[2];
-#pragma unroll
-    for (int x = 0; x < 2; x++) {
-        const uint32_t a1 = P.p0 + w[x][0];
-        const uint32_t a2 = rol32(a1, 5) + P.p1 + w[x][1];
-        const uint32_t a3 = rol32(a2, 5) + f_ch(a1, P.ra, P.rb) + P.p2 + w[x][2];
-        const uint32_t r1 = rol32(a1, 30);
-        const uint32_t a4 = rol32(a3, 5) + f_ch(a2, r1, P.ra) + P.p3 + w[x][3];
-        const uint32_t r2 = rol32(a2, 30);
-        const uint32_t a5 = rol32(a4, 5) + f_ch(a3, r2, r1) + P.p4 + w[x][4];
-        a[x] = a5; b[x] = a4; c[x] = rol32(a3, 30); d[x] = r2; e[x] = r1;
-    }
-#pragma unroll
-    for (int t = 5; t < 80; t++) {
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            uint32_t wt;
-            if (t < 16) {
-                wt = w[x][t];
-            } else {
-                wt = rol32(xor3(w[x][(t - 3) & 15], w[x][(t - 8) & 15], w[x][(t - 14) & 15]) ^ w[x][t & 15], 1);
-                w[x][t & 15] = wt;
-            }
-            uint32_t f, k;
-            if (t < 20)      { f = f_ch(b[x], c[x], d[x]);  k = K; }
-            else if (t < 40) { f = xor3(b[x], c[x], d[x]);  k = 0x6ED9EBA1u; }
-            else if (t < 60) { f = f_maj(b[x], c[x], d[x]); k = 0x8F1BBCDCu; }
-            else             { f = xor3(b[x], c[x], d[x]);  k = 0xCA62C1D6u; }
-            const uint32_t tmp = rol32(a[x], 5) + f + e[x] + (k + wt);
-            e[x] = d[x]; d[x] = c[x]; c[x] = rol32(b[x], 30); b[x] = a[x]; a[x] = tmp;
-        }
-    }
-#pragma unroll
-    for (int x = 0; x < 2; x++) {
-        out[x][0] = st[0] + a[x]; out[x][1] = st[1] + b[x]; out[x][2] = st[2] + c[x]; out[x][3] = st[3] + d[x];
-        out[x][4] = st[4] + e[x];
-    }
 }
 DEVI void sha1_iv(uint32_t st[5]) {
     st[0] = SHA1_IV0; st[1] = SHA1_IV1; st[2] = SHA1_IV2; st[3] = SHA1_IV3; st[4] = SHA1_IV4;

@@ -232,76 +232,6 @@ k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, 
  * and leaves the AES-128 key X1[0:16] of every candidate in HBM ([word][candidate], coalesced);
  * k_office_check does the AES-128 verifier check with its own register budget.  The hand-off costs
  * 32 bytes per candidate against ~3e7 issue slots of hashing. */
-#ifdef OFFICE_KDF_PAIR
-/* round 5 A/B: two candidates per lane (2 g0, 2 g0 + 1), their 50,000 SHA-1s in lockstep (dev_crypto.h
- * sha1_compress2): two independent instruction streams per lane, at 4 waves/SIMD */
-#define OFFICE_PER 2u
-template <int MODE>
-__global__ void __launch_bounds__(256, 4)
-k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
-    __shared__ uint8_t cs[256];
-    __shared__ uint32_t flag;
-    if (!block_prologue<false, false>(e, nullptr, R, stop_on_first, cs, nullptr, &flag, 2u)) return;
-    const uint32_t g0 = 2u * (blockIdx.x * blockDim.x + threadIdx.x);
-    if (g0 >= e.count) return;
-    const uint32_t gg[2] = {g0, g0 + 1u < e.count ? g0 + 1u : g0};
-    uint32_t h[2][5];
-#pragma unroll
-    for (int x = 0; x < 2; x++) {
-        if constexpr (MODE == 2) {
-#pragma unroll
-            for (int k = 0; k < 5; k++) h[x][k] = keys[(size_t)k * e.count + gg[x]];
-        } else {
-            cand c;
-            get_candidate<MODE, true>(e, cs, gg[x], c);
-            uint32_t m[32];
-            m[0] = p.salt[0]; m[1] = p.salt[1]; m[2] = p.salt[2]; m[3] = p.salt[3];
-            be_append<4>(m, c);
-            sha1_msg2(m, 16u + c.len, h[x]);
-        }
-    }
-    for (uint32_t i = 0; i < 50000u; i++) {
-        uint32_t w[2][16], s[2][5];
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const uint32_t m[16] = {bswap32(i), h[x][0], h[x][1], h[x][2], h[x][3], h[x][4], 0x80000000u, 0, 0, 0, 0, 0,
-                                    0, 0, 0, 192u};
-#pragma unroll
-            for (int j = 0; j < 16; j++) w[x][j] = m[j];
-            sha1_iv(s[x]);
-        }
-        sha1_compress2(s, w);
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < 5; k++) h[x][k] = s[x][k];
-    }
-#pragma unroll
-    for (int x = 0; x < 2; x++) {
-        uint32_t hh[5];
-        {
-            uint32_t w[16] = {h[x][0], h[x][1], h[x][2], h[x][3], h[x][4], 0u, 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 192u};
-            sha1_iv(hh);
-            sha1_compress(hh, w);
-        }
-        uint32_t x1[5];
-        {
-            uint32_t w[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) w[j] = 0x36363636u ^ (j < 5 ? hh[j] : 0u);
-            sha1_iv(x1);
-            sha1_compress(x1, w);
-            uint32_t w2[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512u};
-            sha1_compress(x1, w2);
-        }
-        if (x == 0 || g0 + 1u < e.count) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) keys[(size_t)k * e.count + gg[x]] = x1[k];
-        }
-    }
-}
-#else
-#define OFFICE_PER 1u
 template <int MODE>
 __global__ void __launch_bounds__(256, 8)
 k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_on_first, uint32_t *keys) {
@@ -354,7 +284,6 @@ k_office_kdf(dprf_enum e, dprf_office_params p, dprf_results *R, uint32_t stop_o
 #pragma unroll
     for (int k = 0; k < 4; k++) keys[(size_t)k * e.count + g] = x1[k];
 }
-#endif
 
 __global__ void __launch_bounds__(256)
 k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf_results *R, uint32_t cap,
@@ -438,63 +367,6 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
     }
     /* the midstates' message-independent parts of rounds 0-4, once per candidate (dev_crypto.h sha1_pre) */
     const sha1_pre_t ipre = sha1_pre(ist), opre = sha1_pre(ost);
-#ifdef ODT_KDF_PAIR
-    /* round 5 A/B: both output blocks in one loop, their SHA-1s in lockstep (dev_crypto.h sha1_compress_pre2) */
-    {
-        uint32_t u[2][5], t[2][5];
-        {
-            uint32_t w[2][16], s[2][5];
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                const uint32_t m[16] = {p.salt[0], p.salt[1], p.salt[2], p.salt[3], (uint32_t)(x + 1), 0x80000000u,
-                                        0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 20u) * 8u};
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[x][j] = m[j];
-            }
-            sha1_compress_pre2(ist, ipre, w, s);
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                const uint32_t m[16] = {s[x][0], s[x][1], s[x][2], s[x][3], s[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
-                                        0, 0, (64u + 20u) * 8u};
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[x][j] = m[j];
-            }
-            sha1_compress_pre2(ost, opre, w, u);
-        }
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < 5; k++) t[x][k] = u[x][k];
-        for (int it = 1; it < 1024; it++) {
-            uint32_t w[2][16], s[2][5];
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                const uint32_t m[16] = {u[x][0], u[x][1], u[x][2], u[x][3], u[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
-                                        0, 0, (64u + 20u) * 8u};
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[x][j] = m[j];
-            }
-            sha1_compress_pre2(ist, ipre, w, s);
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                const uint32_t m[16] = {s[x][0], s[x][1], s[x][2], s[x][3], s[x][4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0,
-                                        0, 0, (64u + 20u) * 8u};
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[x][j] = m[j];
-            }
-            sha1_compress_pre2(ost, opre, w, u);
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int k = 0; k < 5; k++) t[x][k] ^= u[x][k];
-        }
-#pragma unroll
-        for (int k = 0; k < 5; k++) keys[(size_t)k * e.count + g] = t[0][k];
-#pragma unroll
-        for (int k = 0; k < 3; k++) keys[(size_t)(5 + k) * e.count + g] = t[1][k];
-    }
-    if (true) return;
-#endif
 #pragma unroll
     for (int blkno = 1; blkno <= 2; blkno++) {
         uint32_t u[5], t[5];
@@ -529,88 +401,32 @@ k_odt_kdf(dprf_enum e, dprf_odt_params p, dprf_results *R, uint32_t stop_on_firs
 
 /* The 64 AES-256 block decryptions per candidate read Td0 14,336 times.  A single 1 KiB Td0 puts
  * random indices of 32 lanes on 32 banks (~3.5-way conflicts: 65 % of this kernel's cycles were bank
- * conflicts, profiles/prof_odt_r01.json).  Rounds 1-2 (ODT_SPLIT 0): row x of a 64 KiB table holds Td0[x] in 32
- * dword copies (bytes 0..127, lane l reads copy l%32) and Si[x] in 32 dword copies (bytes 128..255): every lookup
- * conflict-free, its address ONE v_perm of the state byte and the lane's copy offset, but three of a column's four
- * terms rotated (12 v_alignbit per round).
- * Round 3 (ODT_SPLIT 1): R6's split-table scheme (dprf_kernels_r6.hip aes128_encrypt_split) for the inverse cipher:
- * four tables Td_t = ror(Td0, 8t) x 16 copies fill the 256-byte rows, lane group A (bit 4 of the lane clear) reads
+ * conflicts, profiles/prof_odt_r01.json).  The tables follow R6's split-table scheme (dprf_kernels_r6.hip
+ * aes128_encrypt_split; the replicated single table of rounds 1-2, 12 v_alignbit per round, is in HISTORY.md) for
+ * the inverse cipher: four tables Td_t = ror(Td0, 8t) x 16 copies fill the 256-byte rows, lane group A (bit 4 of the lane clear) reads
  * Td_t and group B Td_t+1 in every lookup (32 different banks per 32-lane half), B keeps its state rotated -- after
  * inner round r its register j holds ror(s_(j + rho_r), 8 eps_r) with (rho, eps) -> (rho - eps, eps + 1) for the
  * inverse cipher's column order -- and its round keys are permuted to match; no rotates are left.  Si sits in one
  * more row (address 0x10000 + x, one v_perm; the last round's 16 byte reads share its banks).
  * tests/test_odt_split_model.py restates it against FIPS-197. */
-#ifndef ODT_SPLIT
-#define ODT_SPLIT 1
-#endif
 #define ODT_TD_ROW 256
-__shared__ __attribute__((aligned(16))) uint32_t odt_td[(256 + ODT_SPLIT) * ODT_TD_ROW / 4];
+__shared__ __attribute__((aligned(16))) uint32_t odt_td[(256 + 1) * ODT_TD_ROW / 4];
 
-template <int K>
-DEVI uint32_t tdrep(uint32_t v, uint32_t lanec) {
-    const uint32_t a = __builtin_amdgcn_perm(v, lanec, 0x0c0c0000u | ((4u + K) << 8));
-    return *(const uint32_t *)((const uint8_t *)odt_td + a);
-}
-template <int K>
-DEVI uint32_t isbrep(uint32_t v, uint32_t lanec) {
-    const uint32_t a = __builtin_amdgcn_perm(v, lanec, 0x0c0c0000u | ((4u + K) << 8));
-    return ((const uint8_t *)odt_td)[a + 128u];
-}
-/* aes_decrypt<14> on the replicated table */
-DEVI void aes256_decrypt_rep(const uint32_t *dk, const uint32_t in[4], uint32_t out[4], uint32_t lanec) {
-    uint32_t s0 = in[0] ^ dk[0], s1 = in[1] ^ dk[1], s2 = in[2] ^ dk[2], s3 = in[3] ^ dk[3];
-#pragma unroll
-    for (int r = 1; r < 14; r++) {
-        uint32_t t0 = xor3(xor3(tdrep<3>(s0, lanec), ror32(tdrep<2>(s3, lanec), 8), ror32(tdrep<1>(s2, lanec), 16)),
-                           ror32(tdrep<0>(s1, lanec), 24), dk[4 * r + 0]);
-        uint32_t t1 = xor3(xor3(tdrep<3>(s1, lanec), ror32(tdrep<2>(s0, lanec), 8), ror32(tdrep<1>(s3, lanec), 16)),
-                           ror32(tdrep<0>(s2, lanec), 24), dk[4 * r + 1]);
-        uint32_t t2 = xor3(xor3(tdrep<3>(s2, lanec), ror32(tdrep<2>(s1, lanec), 8), ror32(tdrep<1>(s0, lanec), 16)),
-                           ror32(tdrep<0>(s3, lanec), 24), dk[4 * r + 2]);
-        uint32_t t3 = xor3(xor3(tdrep<3>(s3, lanec), ror32(tdrep<2>(s2, lanec), 8), ror32(tdrep<1>(s1, lanec), 16)),
-                           ror32(tdrep<0>(s0, lanec), 24), dk[4 * r + 3]);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    const uint32_t *r = dk + 56;
-    out[0] = ((isbrep<3>(s0, lanec) << 24) | (isbrep<2>(s3, lanec) << 16) | (isbrep<1>(s2, lanec) << 8) | isbrep<0>(s1, lanec)) ^ r[0];
-    out[1] = ((isbrep<3>(s1, lanec) << 24) | (isbrep<2>(s0, lanec) << 16) | (isbrep<1>(s3, lanec) << 8) | isbrep<0>(s2, lanec)) ^ r[1];
-    out[2] = ((isbrep<3>(s2, lanec) << 24) | (isbrep<2>(s1, lanec) << 16) | (isbrep<1>(s0, lanec) << 8) | isbrep<0>(s3, lanec)) ^ r[2];
-    out[3] = ((isbrep<3>(s3, lanec) << 24) | (isbrep<2>(s2, lanec) << 16) | (isbrep<1>(s1, lanec) << 8) | isbrep<0>(s0, lanec)) ^ r[3];
-}
-
-#if ODT_SPLIT
 /* B's representation (rho, eps) after inner round r = 0..13 of the inverse cipher */
 __device__ constexpr int ODT_RHO[14] = {0, 0, 3, 1, 2, 2, 1, 3, 0, 0, 3, 1, 2, 2};
 __device__ constexpr int ODT_EPS[14] = {0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3, 0, 1};
 #define ODT_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
 /* One inner round: 16 lookups issued column by column (column j: s_j, s_j-1, s_j-2, s_j-3 for lookups t = 0..3),
  * then each column's two v_bitop3 behind the wait covering its reads (as r6_round_asm). */
-/* ODT_B1_BITOP3 (round 4, as R6_B1_BITOP3 in dprf_kernels_r6.hip): the four byte-1 lookups of a round address their
- * table by one full-rate v_bitop3 (s & 0xff00) | (base >> 16 without its byte 1) instead of a half-rate v_perm;
- * base >> 16 is formed in t[15]'s register, whose own lookup comes last.  Measured neutral on ODF (1025.7 vs 1025.5 ms
- * per 16 Mi-candidate step, profiles/ab_odt_b1_bitop3_r04v.txt: the check is ~2.4 % of a step), so off. */
-#ifndef ODT_B1_BITOP3
-#define ODT_B1_BITOP3 0
-#endif
 DEVI void odt_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
                         uint32_t k1, uint32_t k2, uint32_t k3) {
     uint32_t t[16];
 #define ODL(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
-#if ODT_B1_BITOP3
-#define ODT_B2PRE "v_lshrrev_b32 %19, 16, %20\n\t"
-#define ODL2(d, s) "v_bitop3_b32 %" #d ", %" #s ", %29, %19 bitop3:0xe2\n\tds_read_b32 %" #d ", %" #d "\n\t"
-#define ODT_B2IN , "s"(0xff00u)
-#else
-#define ODT_B2PRE
-#define ODL2(d, s) ODL(d, s, 27)
-#define ODT_B2IN
-#endif
     asm volatile(
-        ODT_B2PRE
-        ODL(4, 0, 25) ODL(5, 3, 26) ODL2(6, 2) ODL(7, 1, 28)
-        ODL(8, 1, 25) ODL(9, 0, 26) ODL2(10, 3) ODL(11, 2, 28)
-        ODL(12, 2, 25) ODL(13, 1, 26) ODL2(14, 0) ODL(15, 3, 28)
-        ODL(16, 3, 25) ODL(17, 2, 26) ODL2(18, 1) ODL(19, 0, 28)
+        ODL(4, 0, 25) ODL(5, 3, 26) ODL(6, 2, 27) ODL(7, 1, 28)
+        ODL(8, 1, 25) ODL(9, 0, 26) ODL(10, 3, 27) ODL(11, 2, 28)
+        ODL(12, 2, 25) ODL(13, 1, 26) ODL(14, 0, 27) ODL(15, 3, 28)
+        ODL(16, 3, 25) ODL(17, 2, 26) ODL(18, 1, 27) ODL(19, 0, 28)
         "s_waitcnt lgkmcnt(12)\n\t"
         "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
         "v_bitop3_b32 %0, %4, %7, %21 bitop3:0x96\n\t"
@@ -627,11 +443,8 @@ DEVI void odt_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, 
           "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
           "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
         : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(ODT_SEL(0)), "s"(ODT_SEL(1)), "s"(ODT_SEL(2)),
-          "s"(ODT_SEL(3)) ODT_B2IN
+          "s"(ODT_SEL(3))
         : "memory");
-#undef ODT_B2IN
-#undef ODT_B2PRE
-#undef ODL2
 #undef ODL
 }
 /* Si[byte K of v] from the row after the tables (address 0x10000 + x) */
@@ -668,7 +481,6 @@ DEVI void aes256_decrypt_split(const uint32_t *dk, const uint32_t in[4], uint32_
 #pragma unroll
     for (int j = 0; j < 4; j++) out[j] = perm(acc[j], acc[(j + 3) & 3], selr);
 }
-#endif
 
 #define ODT_CHECK_THREADS 512
 __global__ void __launch_bounds__(ODT_CHECK_THREADS, 4)   /* 2 workgroups (64 KiB table each) per CU */
@@ -679,10 +491,9 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     __shared__ uint32_t flag;
     for (uint32_t k = threadIdx.x; k < 256u * ODT_TD_ROW / 4; k += blockDim.x) {
         const uint32_t x = k >> 6, c = k & 63u;
-        if (ODT_SPLIT) odt_td[k] = ror32(T->td0[x], 8u * (c >> 4));               /* Td_(c/16), copy c % 16 */
-        else odt_td[k] = c < 32u ? T->td0[x] : (uint32_t)T->inv_sbox[x];
+        odt_td[k] = ror32(T->td0[x], 8u * (c >> 4));                             /* Td_(c/16), copy c % 16 */
     }
-    if (ODT_SPLIT && threadIdx.x < 64u) {
+    if (threadIdx.x < 64u) {
         const uint32_t x = 4u * threadIdx.x;                                     /* the Si row at 0x10000 */
         odt_td[256u * ODT_TD_ROW / 4 + threadIdx.x] = (uint32_t)T->inv_sbox[x] | ((uint32_t)T->inv_sbox[x + 1] << 8) |
                                                      ((uint32_t)T->inv_sbox[x + 2] << 16) | ((uint32_t)T->inv_sbox[x + 3] << 24);
@@ -690,11 +501,11 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     if (!block_prologue<true>(e, T, R, stop_on_first, cs, &L, &flag)) return;
     /* odt_round_asm uses the v_perm result as the whole LDS address: the table must sit at LDS address 0 (checked;
      * a build that ever breaks this fails loudly instead of computing wrong) */
-    if (ODT_SPLIT && (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)odt_td != 0u) {
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)odt_td != 0u) {
         if (threadIdx.x == 0) atomicOr(&R->pad_, 4u);
         return;
     }
-    const uint32_t lanec = (threadIdx.x & (ODT_SPLIT ? 15u : 31u)) << 2;
+    const uint32_t lanec = (threadIdx.x & 15u) << 2;
     /* split tables: byte t = row offset of the copy lookup t reads (A: Td_t, B: Td_t+1) */
     const uint32_t base = lanec * 0x01010101u + ((threadIdx.x & 16u) ? 0x00c08040u : 0xc0804000u);
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -706,12 +517,8 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
     uint32_t rk[60], dk[60];
     aes256_expand(L, key, rk);
     aes_dec_schedule<14>(L, rk, dk);
-#if ODT_SPLIT
     odt_dk_split(dk, base);
 #define ODT_DECRYPT(dk, ct, pt) aes256_decrypt_split(dk, ct, pt, base)
-#else
-#define ODT_DECRYPT(dk, ct, pt) aes256_decrypt_rep(dk, ct, pt, lanec)
-#endif
     bool ok;
     if (p.enc_len == 16u) {
         /* experimental 2-byte check (:98-101) */
@@ -1023,11 +830,6 @@ DEVI void r24_key(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *c
 #ifndef R24_PRIO
 #define R24_PRIO 3
 #endif
-/* 1: charset, PAD and the skip flag in an LDS area beside the S-boxes (16,720 B per workgroup, 9 per CU); 0: the
- * S-box area is all the LDS a workgroup takes (16,384 B, 10 per CU) */
-#ifndef R24_LDS_AUX
-#define R24_LDS_AUX 1
-#endif
 /* 1: the KSA as the generated asm block (rc4_dev.h rc4_ksa_asm); 0: the C++ rc4_ksa (A/B builds) */
 #ifndef R24_KSA_ASM
 #define R24_KSA_ASM 1
@@ -1038,26 +840,12 @@ DEVI void r24_ksa(uint8_t *S, uint32_t sbase, uint32_t lane, const uint32_t k[4]
     else rc4_ksa<NK>(S, lane << 2, k);
 }
 template <int R> struct r24_batches { static constexpr uint32_t v = R == 2 ? R2_BATCHES : R34_BATCHES; };
-#ifdef DPRF_DEBUG_R24
-/* Debug builds only (round 5, tools/r24_dump.py): workgroup 0, batch 0 of k_pdf_r24 R3/R4 records its keys, the data
- * words after every pass of both sweeps and lane 0's S-box after each pass of sweep 0, so a wrong verdict on the
- * hardware can be traced to the first pass / KSA that differs from a CPU RC4 chain.  Layout (words):
- * [0, 256) h[4] per lane; [256, 10496) d[4] per (sweep, pass, lane); [10496, 11776) S-box of lane 0 per sweep-0 pass
- * (64 words each); [11776] the number of sweeps run. */
-#define R24_DBG_WORDS 11784
-__device__ uint32_t g_r24_dbg[R24_DBG_WORDS];
-extern "C" int dprf_debug_r24_read(uint32_t *out, size_t nwords) {
-    if (nwords > R24_DBG_WORDS) nwords = R24_DBG_WORDS;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_r24_dbg), nwords * 4, 0, hipMemcpyDeviceToHost);
-}
-#endif
 template <int MODE, int R, int NK>
 __global__ void __launch_bounds__(128, 5)   /* 18 waves per CU (9 workgroups): <= 102 VGPRs */
 k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32_t stop_on_first) {
     constexpr uint32_t NBAT = r24_batches<R>::v;
     static_assert(NBAT % 2 == 0, "block_prologue counts NBAT / 2 candidates per thread of the 128-thread block");
     __shared__ __attribute__((aligned(16))) uint8_t S[RC4_WAVE_BYTES];
-#if R24_LDS_AUX
     __shared__ __attribute__((aligned(16))) uint32_t aux[64 + 16 + 4];
     uint8_t *cs = (uint8_t *)aux;                         /* charset, 256 B */
     uint32_t *padw = aux + 64;                            /* PAD || PAD */
@@ -1065,15 +853,6 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
     if (threadIdx.x < 8) { padw[threadIdx.x] = p.pad[threadIdx.x]; padw[threadIdx.x + 8] = p.pad[threadIdx.x]; }
     /* per = candidates per thread of the 128-thread block: 64 * NBAT candidates */
     if (!block_prologue<false>(e, nullptr, R_, stop_on_first, cs, nullptr, flag, NBAT / 2)) return;
-#else
-    /* the S-box area is the workgroup's only LDS (16,384 B: 10 workgroups per 160 KiB CU); the key wave reads the
-     * charset and PAD from the kernel arguments, and the skip flag passes through the S-box area before the first
-     * batch barrier (every wave reads it before that barrier, the key wave writes keys only after it) */
-    const uint8_t *cs = e.charset;
-    const uint32_t *padw = p.pad;
-    uint32_t *flag = (uint32_t *)S;
-    if (!block_prologue<false, true, false>(e, nullptr, R_, stop_on_first, nullptr, nullptr, flag, NBAT / 2)) return;
-#endif
     const uint32_t base = blockIdx.x * (64u * NBAT);
     const uint32_t left = e.count - base;                 /* > 0: grid = ceil(count / (64 * NBAT)) */
     const uint32_t nb = left >= 64u * NBAT ? (uint32_t)NBAT : (left + 63u) / 64u;
@@ -1116,20 +895,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
         return;
     }
     /* RC4 wave */
-#ifdef R24_PRIO_SPLIT
-    /* round 5 A/B: the RC4 waves of a CU at R24_PRIO_SPLIT different priorities (3, 2, ... by workgroup), all above the
-     * key waves: under issue contention a chain's rate is 1 / its group latency, and by convexity a spread of latencies
-     * around the same mean serves more groups than equal ones (tools/rc4_probe_pmc.py: at 9 waves per CU 22 % of a chain's
-     * wave-cycles are "ready, not issued") */
-    {
-        const uint32_t lvl = blockIdx.x % (uint32_t)R24_PRIO_SPLIT;
-        if (lvl == 0) __builtin_amdgcn_s_setprio(3);
-        else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(1);
-    }
-#else
     __builtin_amdgcn_s_setprio(R24_PRIO);
-#endif
     uint8_t *Sw = S;
     /* the asm KSA needs the S-box area at an LDS address with zero low 16 bits (rc4_ksa_asm); S is this kernel's
      * first LDS object, at 0 -- checked, and a launch that ever breaks it fails loudly instead of computing wrong */
@@ -1178,14 +944,14 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
             uint32_t d[4] = {p.h2[0], p.h2[1], p.h2[2], p.h2[3]};
             /* the asm KSA's key registers, made once per candidate; pass x's key (key ^ x) by XORing x ^ (x - 1)
              * into their byte 0 (16 v_xor per pass, the same count as forming kx and extracting its bytes) */
-            uint32_t kb[rc4_nkr<NK>::v];
+            uint32_t kb[NK];
             rc4_kb_init<NK>(h, kb);
             for (uint32_t x = 0; x < 20u; x++) {
                 if (R24_KSA_ASM) {
                     const uint32_t dx = x ^ (x - 1u);
                     if (x) {
 #pragma unroll
-                        for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+                        for (int q = 0; q < NK; q++) kb[q] ^= dx;
                     }
                     rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
                 } else {
@@ -1193,25 +959,8 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
                     uint32_t kx[4] = {h[0] ^ xx, h[1] ^ xx, h[2] ^ xx, h[3] ^ xx};
                     rc4_ksa<NK>(Sw, lane << 2, kx);
                 }
-#ifdef DPRF_DEBUG_R24
-                if (blockIdx.x == 0 && b == 0 && !full) {
-                    if (x == 0) {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) g_r24_dbg[4 * lane + q] = h[q];
-                    }
-                    if (lane == 0)
-                        for (int w = 0; w < 64; w++) g_r24_dbg[10496 + 64 * x + w] = *(const uint32_t *)(Sw + 256 * w);
-                }
-#endif
                 if (full) rc4_prga<16>(Sw, lane << 2, d);
                 else rc4_prga<2>(Sw, lane << 2, d);
-#ifdef DPRF_DEBUG_R24
-                if (blockIdx.x == 0 && b == 0) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) g_r24_dbg[256 + ((full * 20u + x) * 64u + lane) * 4u + q] = d[q];
-                    if (lane == 0) g_r24_dbg[11776] = full + 1u;
-                }
-#endif
             }
             if (full) {
                 ok = d[0] == p.u[0] && d[1] == p.u[1] && d[2] == p.u[2] && d[3] == p.u[3];
@@ -1233,9 +982,9 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
 hipError_t launch_office(const dprf_enum &e, const dprf_office_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s, uint32_t *keys,
                          hipEvent_t mid) {
-    if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
-    else if (e.mode == 1) hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
-    else hipLaunchKernelGGL(k_office_kdf<2>, GRID(e.count, 256 * OFFICE_PER), dim3(256), 0, s, e, p, R, stop, keys);
+    if (e.mode == 0) hipLaunchKernelGGL(k_office_kdf<0>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else if (e.mode == 1) hipLaunchKernelGGL(k_office_kdf<1>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
+    else hipLaunchKernelGGL(k_office_kdf<2>, GRID(e.count, 256), dim3(256), 0, s, e, p, R, stop, keys);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL(k_office_check, GRID(e.count, 256), dim3(256), 0, s, e, p, T, R, cap, stop, keys);
     return hipGetLastError();

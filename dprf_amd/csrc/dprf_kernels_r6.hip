@@ -557,13 +557,7 @@ template <bool UNI>
 DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hsel, uint32_t K[16], uint32_t colbytes) {
     uint32_t Lp = len + bs;
     if (UNI) Lp = __builtin_amdgcn_readfirstlane(Lp);
-#if R6_PROBE_LANECOL
-    /* timing / PMC probe only (wrong results): the blocks are read from the column of the LANE's index instead of the
-     * slot's, so a 32-lane half meets 32 banks -- what the period-column bank conflicts cost */
-    const uint32_t colbase = UNI ? S.pat + ((opaque_lane() & 63u) << 2) : S.pat + S.lanebase;
-#else
     const uint32_t colbase = S.pat + S.lanebase;                 /* pat is only 16-byte aligned */
-#endif
     r6_load_k(S, len, K);
     /* AES-128 key K[0:16], iv K[16:32] (:259-261) */
     uint32_t rk[44];
@@ -656,7 +650,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
  * 64 queued slots of the fullest class (bitmap words, atomicAnd) and runs one round of them.  Waves
  * never wait for each other.  The previous schedule -- all slots sorted per interval, batches listed
  * costliest first, a workgroup barrier per interval -- left 16 % of wave time at the barriers
- * (-DDPRF_R6_TIMING): ~20 batches of 1-2 M cycles over 12 waves leave a long tail every interval.
+ * (a round-2 per-wave cycle count): ~20 batches of 1-2 M cycles over 12 waves leave a long tail every interval.
  *
  * Deadlock freedom (the round-1 lock-based queue hung): there is no lock and no wave ever waits on a value
  * only another waiting wave could produce.  Every claim is one wave-uniform pass (lane 0's decisions
@@ -678,16 +672,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #endif
 #define R6_SLOTS_PER_THREAD ((R6_MAX_SLOTS + R6_LANES - 1) / R6_LANES)
 #define R6_CLASSES 6
-/* Deferred candidate starts (A/B option, round 3): a slot whose candidate finishes is queued in a seventh queue
- * instead of starting its next candidate inside the round's batch, where the SHA-256 of a new candidate runs for the
- * one or two lanes that finished.  A wave takes that queue as its batch once R6_START_BATCH slots wait in it (or when
- * nothing else is queued).  Measured on MI355X: 3.674 vs 3.683 M cand/s at 16 (the build spills 16 B/lane), so the
- * lane idleness left (VALUUtilization 0.947) is not these starts; off by default. */
-#ifndef R6_START_BATCH
-#define R6_START_BATCH 0
-#endif
-#define R6_QUEUES (R6_CLASSES + (R6_START_BATCH ? 1 : 0))
-#define R6_START_Q R6_CLASSES
+#define R6_QUEUES R6_CLASSES
 #define R6_MAP_WORDS ((R6_MAX_SLOTS + 31) / 32)
 #define R6_IDLE 0xffffffffu
 #ifndef R6_WATCHDOG_S
@@ -695,7 +680,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
 #endif
 
 struct r6_shared {
-    uint32_t map[R6_QUEUES][R6_MAP_WORDS];    /* queued slots of each class (+ the start queue), a bit per slot */
+    uint32_t map[R6_QUEUES][R6_MAP_WORDS];    /* queued slots of each class, a bit per slot */
     uint32_t count[R6_QUEUES];                /* queued slots per queue (a hint for picking one)       */
     uint32_t live;                            /* slots holding a candidate                             */
     uint32_t nslots, te_slots, ncand, pat_words;
@@ -791,179 +776,12 @@ DEVI void r6_push(r6_shared *sh, const r6_lds &S, uint32_t slot) {
 }
 
 
-/* Reserving claims (round 4 A/B, R6_RESERVE): the claim above reads the class counts as a hint and decrements after it
- * has taken its bits, so two waves that pick the same class at the same time split its slots -- one of them then runs a
- * whole round (~10^5 issue slots) for a handful of lanes.  Here lane 0 first RESERVES min(count, 64) slots of the class
- * with a compare-and-swap on its count, and the wave then takes exactly that many bits, scanning again if a racing wave
- * took bits it had chosen.  Termination: a push sets its bit before it increments the count and a claim decrements the
- * count before it clears bits, so at every moment the set bits are at least the count, and every reservation (made
- * against the count) has its bits. */
-#ifndef R6_RESERVE
-#define R6_RESERVE 0
-#endif
-#ifndef R6_RESERVE_PASSES
-#define R6_RESERVE_PASSES 2
-#endif
-#if R6_RESERVE
-DEVI uint32_t r6_claim_reserved(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t best) {
-    uint32_t k = 0;
-    if (lane == 0) {
-        uint32_t old = lds_load(&sh->count[best]);
-        while (old > 0u) {
-            const uint32_t want = old < 64u ? old : 64u;
-            const uint32_t seen = atomicCAS(&sh->count[best], old, old - want);
-            if (seen == old) { k = want; break; }
-            old = seen;
-        }
-    }
-    k = __builtin_amdgcn_readlane(k, 0);
-    if (k == 0u) return 0;
-    /* one pass over the bitmap for the k reserved slots, then (R6_RESERVE_PASSES 2) a second one for what a racing
-     * wave took first; a reservation still unfilled after that is given back to the count */
-    uint32_t total = 0;
-#pragma unroll
-    for (int pass = 0; pass < R6_RESERVE_PASSES; pass++) {
-        if (total >= k) break;                           /* uniform */
-        const uint32_t need = k - total;
-        const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
-        const uint32_t pc = __builtin_popcount(w);
-        uint32_t inc = pc;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(inc, d, 64);
-            if (lane >= (uint32_t)d) inc += o;
-        }
-        uint32_t take = 0u;
-        if (inc <= need) {
-            take = w;
-        } else if (inc - pc < need) {
-            for (uint32_t q = need - (inc - pc), rest = w; q; q--) {
-                take |= rest & (0u - rest);
-                rest &= rest - 1u;
-            }
-        }
-        const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
-        const uint32_t ng = __builtin_popcount(got);
-        uint32_t off = ng;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(off, d, 64);
-            if (lane >= (uint32_t)d) off += o;
-        }
-        const uint32_t pass_total = __builtin_amdgcn_readlane(off, 63);
-        off = total + off - ng;
-        for (uint32_t b = got; b; b &= b - 1u) sh->stage[wave][off++] = (uint16_t)(lane * 32u + __builtin_ctz(b));
-        total += pass_total;
-    }
-    if (lane == 0 && total < k) atomicAdd(&sh->count[best], k - total);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
-    *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
-    return total;
-}
-#endif
-
-/* Bank-placed claims (round 4 A/B, R6_BANK_PLACE): the blocks of a round are read from the slot's period column, which
- * sits in LDS bank slot % 32 (slot_lds: column 4 * (slot % 64), or 128 + 4 * (slot % 32), in rows of 256 bytes); two
- * lanes of one 32-lane half whose slots share that residue conflict on every period read (3.3 % of the CU cycles, 1.3 %
- * of the time: R6_PROBE_LANECOL).  Bit b of every bitmap word is a slot of residue b, so this claim takes, per residue,
- * the first two queued slots of the class (over the words in order: at most 64, no two of a residue in one half) and
- * places the first on lane b, the second on lane 32 + b; if that leaves room it fills the free lanes with further queued
- * slots (those share a bank with a lane of their half).  Race and termination as in r6_claim: atomicAnd tells each word
- * which chosen bits it got, every bit got is placed on a lane, unplaced lanes stay idle. */
-#ifndef R6_BANK_PLACE
-#define R6_BANK_PLACE 0
-#endif
-#ifndef R6_BANK_PLACE_FILL
-#define R6_BANK_PLACE_FILL 1      /* fill the lanes the first-two rule leaves free with further queued slots */
-#endif
-#if R6_BANK_PLACE
-DEVI uint32_t r6_wave_or(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
-    return v;
-}
-DEVI uint32_t r6_scan_add(uint32_t lane, uint32_t v) {    /* inclusive */
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += o;
-    }
-    return v;
-}
-DEVI uint32_t r6_claim_placed(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t best) {
-    const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
-    /* inclusive scan of (residues seen at least once, at least twice) over the words */
-    uint32_t s1 = w, s2 = 0u;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o1 = __shfl_up(s1, d, 64), o2 = __shfl_up(s2, d, 64);
-        if (lane >= (uint32_t)d) { s2 = s2 | o2 | (s1 & o1); s1 = s1 | o1; }
-    }
-    uint32_t e1 = __shfl_up(s1, 1, 64), e2 = __shfl_up(s2, 1, 64);
-    if (lane == 0) { e1 = 0u; e2 = 0u; }
-    const uint32_t r0 = w & ~e1, r1 = w & e1 & ~e2, ov = w & e2;
-    /* the first two of every residue (at most 64 in all), then further slots in word order while lanes are left */
-    /* one scan for both counts: the first-two slots (<= 64) in the low half, the others (<= R6_MAX_SLOTS) above */
-    const uint32_t pco = (uint32_t)__builtin_popcount(ov);
-    const uint32_t sc = r6_scan_add(lane, (uint32_t)__builtin_popcount(r0 | r1) | (pco << 16));
-    const uint32_t room = 64u - (__builtin_amdgcn_readlane(sc, 63) & 0xffffu), inc = sc >> 16;
-    uint32_t tov = 0u;
-    if (!R6_BANK_PLACE_FILL) {
-    } else if (inc <= room) {
-        tov = ov;
-    } else if (inc - pco < room) {
-        for (uint32_t k = room - (inc - pco), rest = ov; k; k--) {
-            tov |= rest & (0u - rest);
-            rest &= rest - 1u;
-        }
-    }
-    const uint32_t take = r0 | r1 | tov;
-    const uint32_t got = take ? (atomicAnd(&sh->map[best][lane], ~take) & take) : 0u;
-    const uint32_t g0 = got & r0, g1 = got & r1, gov = got & tov;
-    const uint32_t nov = (uint32_t)__builtin_popcount(gov);
-    const uint32_t sg = r6_scan_add(lane, (uint32_t)__builtin_popcount(got) | (nov << 16));
-    const uint32_t total = __builtin_amdgcn_readlane(sg, 63) & 0xffffu;
-    if (total == 0u) return 0;
-    sh->stage[wave][lane] = (uint16_t)0xffffu;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    for (uint32_t b = g0; b; b &= b - 1u) {
-        const uint32_t r = (uint32_t)__builtin_ctz(b);
-        sh->stage[wave][r] = (uint16_t)(lane * 32u + r);
-    }
-    for (uint32_t b = g1; b; b &= b - 1u) {
-        const uint32_t r = (uint32_t)__builtin_ctz(b);
-        sh->stage[wave][32u + r] = (uint16_t)(lane * 32u + r);
-    }
-    const uint32_t novt = __builtin_amdgcn_readlane(sg, 63) >> 16;           /* further slots got, wave total */
-    if (novt) {
-        const uint32_t u0 = r6_wave_or(g0), u1 = r6_wave_or(g1);
-        uint64_t fr = ~(((uint64_t)u1 << 32) | (uint64_t)u0);              /* lanes no residue owner took */
-        /* the k-th further slot (word order) on the k-th free lane: a uniform walk over the free lanes */
-        uint32_t j = (sg >> 16) - nov, rest = gov;
-        for (uint32_t k = 0; k < novt; k++) {
-            const uint32_t p = (uint32_t)__builtin_ctzll(fr);
-            fr &= fr - 1ull;
-            if (rest && j == k) {
-                sh->stage[wave][p] = (uint16_t)(lane * 32u + (uint32_t)__builtin_ctz(rest));
-                rest &= rest - 1u;
-                j++;
-            }
-        }
-    }
-    if (lane == 0) atomicSub(&sh->count[best], total);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");       /* stage writes -> reads; bits -> slot state */
-    const uint32_t st = sh->stage[wave][lane];
-    *slot = st == 0xffffu ? R6_IDLE : st;
-    return total;
-}
-#endif
-
 /* Wave-uniform: claim up to 64 queued slots of the fullest class; returns how many (0: none queued) and
  * this lane's slot in *slot.  Lane w < R6_MAP_WORDS owns bitmap word w; lanes take their words' bits in
  * order up to 64 in total, clear exactly the bits they chose (atomicAnd returns what they got when another
  * wave raced them), and the ids are handed out through the wave's stage row. */
 template <int MODE>
-DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot, uint32_t *queue) {
+DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *slot) {
     const uint32_t cnt = lane < R6_QUEUES ? lds_load(&sh->count[lane]) : 0u;
     uint32_t best = R6_CLASSES, bc = 0;
 #pragma unroll
@@ -971,21 +789,7 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
         const uint32_t v = __builtin_amdgcn_readlane(cnt, c);
         if (v > bc) { bc = v; best = c; }
     }
-#if R6_START_BATCH
-    {
-        const uint32_t vs = __builtin_amdgcn_readlane(cnt, R6_START_Q);
-        if (vs >= R6_START_BATCH || (bc == 0 && vs > 0)) { bc = vs; best = R6_START_Q; }
-    }
-#endif
-    *queue = best;
     if (bc == 0) return 0;
-#if R6_RESERVE
-    /* range mode only: the list-mode instantiations spill 12 B/lane with it at the 168-VGPR limit */
-    if (MODE == 0 && best < R6_CLASSES) return r6_claim_reserved(sh, lane, wave, slot, best);
-#endif
-#if R6_BANK_PLACE
-    if (MODE == 0 && best < R6_CLASSES) return r6_claim_placed(sh, lane, wave, slot, best);
-#endif
     const uint32_t w = lane < R6_MAP_WORDS ? lds_load(&sh->map[best][lane]) : 0u;
     const uint32_t pc = __builtin_popcount(w);
     /* inclusive scan of the word popcounts over the wave */
@@ -1024,14 +828,6 @@ DEVI uint32_t r6_claim(r6_shared *sh, uint32_t lane, uint32_t wave, uint32_t *sl
     *slot = lane < total ? sh->stage[wave][lane] : R6_IDLE;
     return total;
 }
-#ifdef DPRF_R6_TIMING
-/* debug builds (-DDPRF_R6_TIMING): per-wave cycles in rounds vs waiting for queued slots */
-#define R6T_DECL unsigned long long t_work = 0, t_wait = 0, t_x = __builtin_readcyclecounter(), t_nb = 0, t_part = 0;
-#define R6T_MARK(acc) { unsigned long long t_y = __builtin_readcyclecounter(); acc += t_y - t_x; t_x = t_y; }
-#else
-#define R6T_DECL
-#define R6T_MARK(acc)
-#endif
 
 template <int MODE>
 __global__ void __launch_bounds__(R6_LANES, 1)     /* 12 waves/CU: <= 168 VGPRs */
@@ -1080,11 +876,10 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         }
     }
     __syncthreads();
-    R6T_DECL
     if (lane == 0) sh->idle_t0[wave] = 0ull;
     for (;;) {
-        uint32_t slot, queue;
-        const uint32_t n = r6_claim<MODE>(sh, opaque_lane(), wave, &slot, &queue);
+        uint32_t slot;
+        const uint32_t n = r6_claim<MODE>(sh, opaque_lane(), wave, &slot);
         if (n == 0) {
             if (lds_load(&sh->live) == 0u) break;                  /* uniform: one LDS word */
             /* watchdog on the constant-rate wall clock: a wave that has found nothing queued for idle_ticks
@@ -1100,31 +895,9 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                 break;
             }
             __builtin_amdgcn_s_sleep(4);
-            R6T_MARK(t_wait)
             continue;
         }
         if (lane == 0) __hip_atomic_store(&sh->idle_t0[wave], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef DPRF_R6_TIMING
-        t_nb++;
-        t_part += n;
-#endif
-#if R6_START_BATCH
-        if (queue == R6_START_Q) {
-            /* a batch of slots whose candidates finished: they take their next candidates together (one cursor
-             * atomic for the wave), start them and queue their first rounds, or retire when the cursor is dry */
-            if (slot != R6_IDLE) {
-                const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
-                if (r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane())))
-                    r6_push(sh, S, slot);
-                else
-                    atomicSub(&sh->live, 1u);
-            }
-            R6T_MARK(t_work)
-            continue;
-        }
-#else
-        (void)queue;
-#endif
         if (slot != R6_IDLE) {
             const r6_lds S = slot_lds(patbase, pat_words, te_slots, slot, opaque_lane());
             const uint32_t st = sh->state[slot];
@@ -1145,29 +918,15 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                     atomicMin(&R->first, idx);
                     if (stop_on_first) atomicExch(&R->stop, 1u);
                 }
-#if R6_START_BATCH
-                /* to the start queue (the slot stays live until it takes a candidate or retires) */
-                more = false;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                atomicOr(&sh->map[R6_START_Q][slot >> 5], 1u << (slot & 31u));
-                atomicAdd(&sh->count[R6_START_Q], 1u);
-#else
                 /* the finishing lanes of the batch take their next candidates together */
                 more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
                 if (!more) atomicSub(&sh->live, 1u);
-#endif
             } else {
                 sh->state[slot] = len | (bs << 8) | (i << 16);
             }
             if (more) r6_push(sh, S, slot);
         }
-        R6T_MARK(t_work)
     }
-#ifdef DPRF_R6_TIMING
-    if (lane == 0 && blockIdx.x < 2)
-        printf("r6 timing wg %u wave %u: work %llu wait %llu batches %llu slots %llu\n", blockIdx.x, wave, t_work,
-               t_wait, t_nb, t_part);
-#endif
 }
 
 /* Slot capacity of one workgroup: 32-slot groups in the upper halves of the Te0 rows, then 64-slot groups

@@ -3,11 +3,7 @@
 #ifndef DPRF_RC4_DEV_H
 #define DPRF_RC4_DEV_H
 #include "dev_crypto.h"
-#ifdef RC4_KSA_ASM_HEADER            /* A/B builds: a variant of the generated schedule */
-#include RC4_KSA_ASM_HEADER
-#else
 #include "rc4_ksa_asm.h"
-#endif
 
 /* RC4 state: one 256-byte S-box per lane in LDS, laid out so that lane l owns bank l%32 for every
  * byte: S[i] of lane l lives at wave_base + (i>>2)*256 + l*4 + (i&3).  Byte reads/writes of a wave
@@ -112,38 +108,27 @@ DEVI void rc4_ksa(uint8_t *S, uint32_t lanebase, const uint32_t k[4]) {
 }
 
 /* The same KSA as one generated inline-asm block (rc4_ksa_asm.h, tools/gen_rc4_ksa_asm.py: the schedule above in
- * 11 VALU instructions per group of two steps instead of the 16-17 LLVM emits, byte selects as SDWA operands, and
- * -- RC4_KSA_KB_CTR, round 3 -- the compare positions i0 / i1 counted in byte 3 of j itself).
+ * 11 VALU instructions per group of two steps instead of the 16-17 LLVM emits, byte selects as SDWA operands).
  * sbase: LDS address of the wave's 16 KiB area, low 16 bits zero (the SDWA byte-1 insert of the S[j] address
  * overwrites bits 8-15 of lanebase; the caller checks); lanebase = sbase + 4 * lane.  Writes the identity itself
  * and returns with no LDS operation in flight.  kb: the key registers rc4_kb_init makes. */
-#ifndef RC4_KSA_KB_CTR                   /* headers generated before the j counter */
-#define RC4_KSA_KB_CTR 0
-#define RC4_KSA_NKR_5 5
-#endif
-template <int NK> struct rc4_nkr { static constexpr int v = NK == 5 ? RC4_KSA_NKR_5 : NK; };
 
-/* Key registers of the asm KSA from the LE-packed key k[4]: register q holds key byte q % NK in byte 0; with the j
- * counter bytes 1-2 are zero and byte 3 is the counter's step for the parity of the positions it serves (+3 after
- * an even step, -1 after an odd one: byte 3 of j is then i1 after step i0 and i0 after step i1).  Only byte 0 changes
- * when a caller XORs a pass constant < 256 into every register (R3/R4's key ^ x). */
+/* Key registers of the asm KSA from the LE-packed key k[4]: register q holds key byte q in byte 0 (anything above
+ * it: the block reads byte 0 only).  Only byte 0 changes when a caller XORs a pass constant < 256 into every
+ * register (R3/R4's key ^ x). */
 template <int NK>
-DEVI void rc4_kb_init(const uint32_t k[4], uint32_t kb[rc4_nkr<NK>::v]) {
+DEVI void rc4_kb_init(const uint32_t k[4], uint32_t kb[NK]) {
 #pragma unroll
-    for (int q = 0; q < rc4_nkr<NK>::v; q++) {
-        const int p = q % NK;
-        const uint32_t b = k[p >> 2] >> (8 * (p & 3));
-        kb[q] = RC4_KSA_KB_CTR ? ((b & 0xffu) | ((q & 1) ? 0xff000000u : 0x03000000u)) : b;
-    }
+    for (int q = 0; q < NK; q++) kb[q] = k[q >> 2] >> (8 * (q & 3));
 }
 
 template <int NK>
-DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc4_nkr<NK>::v]) {
+DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[NK]) {
     static_assert(NK == 5 || NK == 16, "rc4_ksa_asm.h holds the 5- and 16-byte key schedules");
     uint32_t j, W, x0, x1, v1, a0, a1, m, st, m0s, wn;
-    uint64_t c0, c1, c2, c3, h0;                       /* SGPR pairs of the prefetch variant (A/B headers) */
-    /* the identity by ds_write_b128: lane l writes row 4t + l/16, bytes 16 (l%16) .. +16, for t = 0..15, first
-     * value 0x03020100 + 0x04040404 (l/16) in every dword, +0x10101010 per t (gen_rc4_ksa_asm.py identity_b128) */
+    /* operands the shipped schedule does not read (%8, %11-%15, %18-%20): kept so that the block's register
+     * assignment -- and with it the kernel's machine code -- is the one measured (rounds 3-5 variants used them) */
+    uint64_t c0, c1, c2, c3, h0;
     const uint32_t l4 = lanebase - sbase;                /* 4 * lane */
     const uint32_t ia = sbase + ((l4 >> 6) << 8) + ((l4 & 60u) << 2);
     const uint32_t d0 = 0x03020100u + 0x04040404u * (l4 >> 6);
@@ -152,20 +137,12 @@ DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc
     "=&v"(j), "=&v"(W), "=&v"(x0), "=&v"(x1), "=&v"(v1), "=&v"(a0), "=&v"(a1), "=&v"(m), "=&s"(st), "=&s"(m0s),   \
         "=&v"(wn), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(h0)
 #define RC4_KSA_INS "v"(lanebase), "s"(sbase), "v"(ia), "s"(c16), "v"(d0)
-#define KB(q) "v"(kb[(q) % rc4_nkr<NK>::v])
-    /* A/B headers that merge with one v_perm (gen_rc4_ksa_asm.py --d16merge) read one more constant after the keys */
-#ifdef RC4_KSA_SELHIT
-    const uint32_t selhit = RC4_KSA_SELHIT, selno = RC4_KSA_SELNOHIT;
-#define RC4_KSA_XIN , "v"(selhit), "v"(selno)
-#elif defined(RC4_KSA_IDREGS)
-    /* A/B headers with the first identity rows as inputs (gen_rc4_ksa_asm.py --idregs): loop-invariant constants */
+#define KB(q) "v"(kb[q])
+    /* the first identity rows as inputs: loop-invariant constants */
     uint32_t idc[RC4_KSA_IDREGS];
 #pragma unroll
     for (int w = 0; w < RC4_KSA_IDREGS; w++) idc[w] = 0x03020100u + 0x04040404u * (uint32_t)w;
 #define RC4_KSA_XIN RC4_KSA_IDIN
-#else
-#define RC4_KSA_XIN
-#endif
     if constexpr (NK == 16) {
         asm volatile(RC4_KSA_ASM_16
                      : RC4_KSA_OUTS
@@ -173,14 +150,9 @@ DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc
                        KB(11), KB(12), KB(13), KB(14), KB(15) RC4_KSA_XIN
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     } else {
-        /* the operand count is checked where the template is defined: the variant is chosen by the preprocessor */
         asm volatile(RC4_KSA_ASM_5
                      : RC4_KSA_OUTS
-#if RC4_KSA_NKR_5 == 10
-                     : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4), KB(5), KB(6), KB(7), KB(8), KB(9) RC4_KSA_XIN
-#else
                      : RC4_KSA_INS, KB(0), KB(1), KB(2), KB(3), KB(4) RC4_KSA_XIN
-#endif
                      : "vcc", "memory", "v60", "v61", "v62", "v63");
     }
 #undef RC4_KSA_XIN
@@ -191,7 +163,7 @@ DEVI void rc4_ksa_asm_kb(uint32_t sbase, uint32_t lanebase, const uint32_t kb[rc
 
 template <int NK>
 DEVI void rc4_ksa_asm(uint32_t sbase, uint32_t lanebase, const uint32_t k[4]) {
-    uint32_t kb[rc4_nkr<NK>::v];
+    uint32_t kb[NK];
     rc4_kb_init<NK>(k, kb);
     rc4_ksa_asm_kb<NK>(sbase, lanebase, kb);
 }

@@ -36,39 +36,26 @@ def ref_ksa(key, n):
 
 def emulate(prog, keys, nk, sbase=0, text=None):
     """Run the block for 64 lanes; keys[l] = the lane's key bytes.  Returns the 64 S-boxes.  text: the header the
-    block comes from (its RC4_KSA_KB_CTR says how the kernel fills the key registers)."""
+    block comes from (its RC4_KSA_IDREGS says how many identity rows the kernel passes as inputs)."""
     lds = np.zeros(sbase + 16384, dtype=np.uint8)
     lane = np.arange(LANES, dtype=np.uint64)
     regs = {}
     sregs = {"m0": 0}
     kb = []
-    ctr = re.search(r"#define RC4_KSA_KB_CTR (\d)", text or "")
-    ctr = bool(ctr and ctr.group(1) == "1")
-    nkr = 10 if (ctr and nk == 5) else nk
-    for q in range(nkr):
-        p = q % nk
+    for p in range(nk):
         w = np.array([int.from_bytes(bytes(k[(p & ~3):(p & ~3) + 4]).ljust(4, b"\0"), "little") for k in keys],
                      dtype=np.uint64)
-        w = w >> np.uint64(8 * (p & 3))                   # garbage above byte 0, as the kernel passes raw registers
-        if ctr:                                           # rc4_kb_init: key byte | j-counter step in byte 3
-            w = (w & np.uint64(0xff)) | np.uint64(0xff000000 if q & 1 else 0x03000000)
-        kb.append(w)
+        kb.append(w >> np.uint64(8 * (p & 3)))            # garbage above byte 0, as the kernel passes raw registers
     l4 = 4 * lane
     vin = {"%16": sbase + l4, "%17": sbase,
            "%18": sbase + ((l4 >> np.uint64(6)) << np.uint64(8)) + ((l4 & np.uint64(60)) << np.uint64(2)),
            "%19": 0x1010101010101010, "%20": np.uint64(0x03020100) + np.uint64(0x04040404) * (l4 >> np.uint64(6))}
-    for q in range(nkr):
+    for q in range(nk):
         vin["%%%d" % (21 + q)] = kb[q]
-    sel = re.search(r"#define RC4_KSA_SELHIT (0x[0-9a-f]+)u", text or "")
-    if sel:                                                # the --d16merge input after the key registers
-        vin["%%%d" % (21 + nkr)] = np.full(LANES, int(sel.group(1), 16), dtype=np.uint64)
-        no = re.search(r"#define RC4_KSA_SELNOHIT (0x[0-9a-f]+)u", text)
-        vin["%%%d" % (22 + nkr)] = np.full(LANES, int(no.group(1), 16), dtype=np.uint64)
     idr = re.search(r"#define RC4_KSA_IDREGS (\d+)", text or "")
-    if idr:                                                # --idregs: identity rows as inputs after the key registers
+    if idr:                                                # identity rows as inputs after the key registers
         for w in range(int(idr.group(1))):
-            vin["%%%d" % (21 + nkr + w)] = np.full(LANES, 0x03020100 + 0x04040404 * w, dtype=np.uint64)
-    masks = {}                                             # SGPR pairs written by v_cmp (per-lane booleans)
+            vin["%%%d" % (21 + nk + w)] = np.full(LANES, 0x03020100 + 0x04040404 * w, dtype=np.uint64)
     vcc = np.zeros(LANES, dtype=bool)
     M32 = np.uint64(0xffffffff)
 
@@ -99,13 +86,6 @@ def emulate(prog, keys, nk, sbase=0, text=None):
         last = a[-1].split() if a else []
         if op == "s_mov_b32":
             sregs[a[0]] = s(a[1])
-        elif op == "s_mov_b64":
-            assert a[0] == "vcc"
-            vcc = masks[a[1]].copy()
-        elif op == "s_nop":
-            pass
-        elif op == "s_movk_i32":
-            sregs[a[0]] = int(a[1], 0)
         elif op == "s_waitcnt":
             pass
         elif op == "v_mov_b32":
@@ -117,31 +97,8 @@ def emulate(prog, keys, nk, sbase=0, text=None):
                 lds[addr:addr + 4] = np.frombuffer(int(v(d)[l_]).to_bytes(4, "little"), dtype=np.uint8)
         elif op == "v_add_u32":
             regs[a[0]] = (v(a[1]) + v(a[2])) & M32
-        elif op == "v_lshlrev_b32":                          # dst = src1 << (src0 & 31)
-            regs[a[0]] = (v(a[2]) << (v(a[1]) & np.uint64(31))) & M32
-        elif op == "v_lshrrev_b32":
-            regs[a[0]] = (v(a[2]) & M32) >> (v(a[1]) & np.uint64(31))
-        elif op == "v_bfm_b32":                              # ((1 << src0) - 1) << src1, 5-bit fields
-            w_ = (np.uint64(1) << (v(a[1]) & np.uint64(31))) - np.uint64(1)
-            regs[a[0]] = (w_ << (v(a[2]) & np.uint64(31))) & M32
-        elif op == "v_lshlrev_b32_sdwa":
-            assert "src1_sel:BYTE_0" in ln and "dst_sel:DWORD" in ln and "src0_sel:DWORD" in ln
-            regs[a[0]] = ((v(a[2].split()[0]) & np.uint64(0xff)) << (v(a[1]) & np.uint64(31))) & M32
-        elif op == "ds_mskor_rtn_b32":                       # MEM = (MEM & ~DATA0) | DATA1, old dword returned
-            ad = v(a[1]).astype(np.int64)
-            assert bool(np.all(ad % 4 == 0)), "mskor address not dword-aligned"
-            old = np.zeros(LANES, dtype=np.uint64)
-            for b in range(4):
-                old |= lds[ad + b].astype(np.uint64) << np.uint64(8 * b)
-            new = (old & ~v(a[2]) & M32) | v(a[3])
-            assert bool(np.all(new <= M32))
-            for b in range(4):
-                lds[ad + b] = ((new >> np.uint64(8 * b)) & np.uint64(0xff)).astype(np.uint8)
-            regs[a[0]] = old
         elif op == "v_add3_u32":
             regs[a[0]] = (v(a[1]) + v(a[2]) + v(a[3])) & M32
-        elif op == "v_and_or_b32":
-            regs[a[0]] = (v(a[1]) & v(a[2])) | v(a[3])
         elif op == "v_bitop3_b32":
             lut = int(re.search(r"bitop3:(0x[0-9a-f]+)", ln).group(1), 16)
             x0, x1, x2 = v(a[1]), v(a[2]), v(a[3].split()[0])
@@ -159,53 +116,20 @@ def emulate(prog, keys, nk, sbase=0, text=None):
         elif op == "v_cmp_eq_u32_sdwa":
             assert "src0_sel:BYTE_0" in ln
             src1 = a[2].split()[0]
-            if (src1.startswith("%") or re.match(r"v\d+$", src1)) and src1 not in sregs and \
-                    (src1 not in vin or not isinstance(vin[src1], int)):
-                # a VGPR, byte-selected (BYTE_3 of j: the position counter; BYTE_2/3 of the ic4 constants)
-                sh1 = {"BYTE_0": 0, "BYTE_1": 8, "BYTE_2": 16, "BYTE_3": 24}[re.search(r"src1_sel:(\w+)", ln).group(1)]
+            if src1.startswith("%"):
+                # a VGPR, byte-selected: the (i0, i1) compare constants
+                sh1 = {"BYTE_0": 0, "BYTE_1": 8}[re.search(r"src1_sel:(\w+)", ln).group(1)]
                 r = (v(a[1]) & np.uint64(0xff)) == ((v(src1) >> np.uint64(sh1)) & np.uint64(0xff))
             else:
-                r = (v(a[1]) & np.uint64(0xff)) == np.uint64(s(src1))
-            if a[0] == "vcc":
-                vcc = r
-            else:
-                masks[a[0]] = r
+                r = (v(a[1]) & np.uint64(0xff)) == np.uint64(int(src1, 0))
+            assert a[0] == "vcc"
+            vcc = r
         elif op == "ds_read_u8":
             base, o = a[1].split()[0], off(a[1].split()[1] if len(a[1].split()) > 1 else None)
             regs[a[0]] = lds[(v(base) + np.uint64(o)).astype(np.int64)].astype(np.uint64)
-        elif op in ("ds_read_u8_d16", "ds_read_u8_d16_hi"):
-            b = lds[v(a[1]).astype(np.int64)].astype(np.uint64)
-            old = regs.get(a[0], np.zeros(LANES, dtype=np.uint64))
-            regs[a[0]] = (old & np.uint64(0xffff0000)) | b if op == "ds_read_u8_d16" else (old & np.uint64(0xffff)) | (b << np.uint64(16))
-        elif op == "v_perm_b32":
-            hi_, lo_, sel = v(a[1]), v(a[2]), v(a[3])
-            r = np.zeros(LANES, dtype=np.uint64)
-            for k in range(4):
-                sk = (sel >> np.uint64(8 * k)) & np.uint64(0xff)
-                src = np.where(sk >= 4, hi_, lo_)
-                byte = (src >> (np.uint64(8) * (sk & np.uint64(3)))) & np.uint64(0xff)
-                byte = np.where(sk == 0x0c, np.uint64(0), byte)
-                assert bool(np.all((sk <= 7) | (sk == 0x0c))), "selector values the emulator models: 0-7, 0x0c"
-                r |= byte << np.uint64(8 * k)
-            regs[a[0]] = r
         elif op == "ds_write_b8":
             d, o = a[1].split()[0], off(a[1].split()[1] if len(a[1].split()) > 1 else None)
             lds[(v(a[0]) + np.uint64(o)).astype(np.int64)] = (v(d) & np.uint64(0xff)).astype(np.uint8)
-        elif op == "ds_write_b128":
-            assert a[1].split()[0] == "v[60:63]"
-            o = off(a[1].split()[1]) if len(a[1].split()) > 1 else 0
-            ad = (v(a[0]) + np.uint64(o)).astype(np.int64)
-            for k in range(4):
-                val = regs["v%d" % (60 + k)]
-                for b in range(4):
-                    lds[ad + 4 * k + b] = ((val >> np.uint64(8 * b)) & np.uint64(0xff)).astype(np.uint8)
-        elif op == "v_lshl_add_u64":
-            m = re.match(r"v\[(\d+):(\d+)\]", a[0])
-            lo_, hi_ = "v%s" % m.group(1), "v%s" % m.group(2)
-            assert a[1] == a[0] and a[2] == "0"
-            x = regs[lo_] | (regs[hi_] << np.uint64(32))
-            x = x + np.uint64(s(a[3]))
-            regs[lo_], regs[hi_] = x & M32, x >> np.uint64(32)
         elif op == "ds_read_u16":
             base, o = a[1].split()[0], off(a[1].split()[1])
             ad = (v(base) + np.uint64(o)).astype(np.int64)
@@ -293,44 +217,35 @@ def lds_hazards(prog):
     return out
 
 
-@pytest.mark.parametrize("flag", ["", "--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1", "--ic4", "--split-add", "--split-add --ic4", "--and-or",
-                                  "--idregs 24", "--mskor", "--bytes"])
-def test_schedule_waits_cover_every_lds_result(flag):
-    """Every schedule the GPU ran green reads an LDS result only after an lgkmcnt wait that covers it."""
-    import subprocess
-    import sys
-    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
+def test_schedule_waits_cover_every_lds_result():
+    """The shipped schedule reads an LDS result only after an lgkmcnt wait that covers it."""
+    text = open(HDR).read()
     for nk in (5, 16):
-        assert lds_hazards(program(nk, text)) == [], (flag, nk, lds_hazards(program(nk, text))[:3])
+        assert lds_hazards(program(nk, text)) == [], (nk, lds_hazards(program(nk, text))[:3])
 
 
-@pytest.mark.parametrize("flag", ["--d16merge", "--ic4 --d16merge", "--split-add --ic4 --d16merge"])
-def test_d16_merge_schedule_is_rejected(flag):
-    """Round 4's --d16merge variant computed wrong S-boxes on the MI355X (profiles/ab_r24_d16merge_r04b.log) although
-    emulate() passes it: x1's ds_read_u8_d16_hi into the register x0's ds_read_u8_d16 is still filling reads that
-    register at issue, so the low half it keeps is the stale one.  The hazard model names it."""
-    import subprocess
-    import sys
-    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
-    for nk in (5, 16):
-        hz = lds_hazards(program(nk, text))
-        assert hz and all("d16 load reads its destination at issue" in h for _, h in hz), (flag, nk, hz[:3])
+def test_d16_merge_hazard_is_named():
+    """Round 4's d16-merge schedule (retired, HISTORY.md) computed wrong S-boxes on the MI355X
+    (profiles/ab_r24_d16merge_r04b.log) although its dataflow was right: x1's ds_read_u8_d16_hi into the register x0's
+    ds_read_u8_d16 is still filling reads that register at issue, so the low half it keeps is the stale one.  The hazard
+    model names that pattern (kept so that any future schedule using d16 loads is checked the same way)."""
+    prog = ["ds_read_u8_d16 %2, %5", "ds_read_u8_d16_hi %2, %6", "s_waitcnt lgkmcnt(0)", "v_mov_b32 %7, %2"]
+    hz = lds_hazards(prog)
+    assert len(hz) == 1 and hz[0][0] == 1 and "d16 load reads its destination at issue" in hz[0][1], hz
+    assert lds_hazards(["ds_read_u8_d16 %2, %5", "s_waitcnt lgkmcnt(0)", "ds_read_u8_d16_hi %2, %6",
+                        "s_waitcnt lgkmcnt(0)"]) == []
 
 
 def test_idregs_without_the_m0_wait_state_is_rejected():
-    """The first round-4 --idregs build (identity rows 0..23 from input VGPRs) stored row 0 right behind the M0 write
+    """The first round-4 build with identity rows 0..23 from input VGPRs stored row 0 right behind the M0 write
     and failed the R4 verdict table on the MI355X (gpurun_out/id24_tests.log, 23:39); emulate() passes it.  Round 5
     re-ran that schedule in tools/rc4_ksa_probe.hip on the MI355X (profiles/rc4_ksa_probe_r05.txt): row 0 wrong.  With
-    the wait state (the generator's default since dc0a9da) the probe, the verdict tables and the per-pass trace of
-    tools/r24_dump.py are green (profiles/rc4_ksa_probe_r05.txt)."""
+    the wait state (the generator's default since dc0a9da) the probe, the verdict tables and round 5's per-pass trace
+    of the R3/R4 chain are green (profiles/rc4_ksa_probe_r05.txt)."""
     import subprocess
     import sys
     gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen, "--idregs", "24", "--no-m0-wait"], capture_output=True, text=True,
-                          check=True).stdout
+    text = subprocess.run([sys.executable, gen, "--no-m0-wait"], capture_output=True, text=True, check=True).stdout
     for nk in (5, 16):
         prog = program(nk, text)
         hz = lds_hazards(prog)
@@ -358,36 +273,14 @@ def test_generated_ksa_equals_rc4(nk):
             assert got[l_] == ref_ksa(keys[l_], nk), (nk, trial, l_)
 
 
-@pytest.mark.parametrize("flag", ["--early-read", "--late-merge", "--prefetch", "--salu-consts", "--b128-identity",
-                                  "--jctr", "--early-v1", "--ic4", "--d16merge", "--ic4 --d16merge", "--split-add", "--mskor", "--bytes",
-                                  "--split-add --ic4", "--split-add --ic4 --d16merge", "--and-or", "--idregs 24"])
-def test_schedule_variants_equal_rc4(flag):
-    """The A/B variants of the generator (other instruction orders; the prefetch one reads the next pair before this
-    group's S[j] stores and repairs it) compute the same key schedule."""
-    import subprocess
-    import sys
-    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
-    for nk in (5, 16):
-        rng = random.Random(nk + 100)
-        keys = [[rng.randrange(256) for _ in range(16)] for _ in range(LANES)]
-        keys[0], keys[1], keys[2] = [0] * 16, [1] * 16, [2] * 16
-        got = emulate(program(nk, text), keys, nk, text=text)
-        assert all(got[l_] == ref_ksa(keys[l_], nk) for l_ in range(LANES)), (flag, nk)
-
-
-@pytest.mark.parametrize("flag", ["", "--idregs 24", "--and-or", "--jctr"])
-def test_m0_write_is_not_followed_by_an_lds_instruction(flag):
+def test_m0_write_is_not_followed_by_an_lds_instruction():
     """gfx9 hazard: an instruction that reads M0 (ds_write_addtid_b32) needs one wait state after the s_mov that writes
-    M0; the emulator cannot see it (a variant that stored row 0 right behind the s_mov failed parity on the GPU)."""
-    import subprocess
-    import sys
-    gen = os.path.join(HERE, "..", "tools", "gen_rc4_ksa_asm.py")
-    text = subprocess.run([sys.executable, gen] + flag.split(), capture_output=True, text=True, check=True).stdout
+    M0; the emulator cannot see it (a schedule that stored row 0 right behind the s_mov failed parity on the GPU)."""
+    text = open(HDR).read()
     for nk in (5, 16):
         prog = program(nk, text)
         for a, b in zip(prog, prog[1:]):
-            assert not (a.startswith("s_mov_b32 m0,") and b.startswith("ds_")), (flag, nk, a, b)
+            assert not (a.startswith("s_mov_b32 m0,") and b.startswith("ds_")), (nk, a, b)
 
 
 def test_header_is_what_the_generator_writes():

@@ -3,7 +3,7 @@
 ~177 MB extra in the FIRST k_pdf_r6 dispatch of some processes).
 
 Each run is `rocprofv3 --pmc WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -- python3 bench.py --workload pdf_r6
---steps 1 --warmup 0` (tools/session_r05d.sh).  A context save of the resident waves (CWSR: the scheduler preempting
+--steps 1 --warmup 0` (tools/sessions/session_r05d.sh).  A context save of the resident waves (CWSR: the scheduler preempting
 the queue) writes every wave's VGPRs + SGPRs and every CU's LDS; a restored wave is launched again, so SQ_WAVES of
 that dispatch exceeds its grid.  Printed per dispatch: candidates (from the trace duration share), WRITE bytes per
 candidate, SQ_WAVES, and the expected size of a whole-chip context save from the kernel's resources.

@@ -4,8 +4,8 @@
  * loop (key ^ x, x = 0..PASSES-1, pdf_password_verifier.c:164-176).  The host compares every box with a plain RC4
  * key schedule and prints, per variant header, how many lanes differ and WHERE: the positions that differ, the
  * rows (dword w = positions 4w..4w+3) they sit in, and lane 0's first difference.  Build one executable per header:
- *   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRC4_KSA_ASM_HEADER='"<hdr>"' tools/rc4_ksa_probe.hip -o <exe>
- * (RC4_KSA_IDREGS / RC4_KSA_SELHIT headers are fed by rc4_dev.h's hooks).  Usage: <exe> [blocks] [passes] */
+ *   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/rc4_ksa_probe.hip -o <exe>
+ * (the shipped rc4_ksa_asm.h).  Usage: <exe> [blocks] [passes] */
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -28,13 +28,13 @@ __global__ void __launch_bounds__(64) k_probe(const uint32_t *keys, uint8_t *out
         return;
     }
     uint32_t k[4] = {keys[4 * g], keys[4 * g + 1], keys[4 * g + 2], keys[4 * g + 3]};
-    uint32_t kb[rc4_nkr<NK>::v];
+    uint32_t kb[NK];
     rc4_kb_init<NK>(k, kb);
     for (int x = 0; x < passes; x++) {
         if (x) {
             const uint32_t dx = (uint32_t)x ^ (uint32_t)(x - 1);
 #pragma unroll
-            for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+            for (int q = 0; q < NK; q++) kb[q] ^= dx;
         }
         rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
         if (x == 0 || x == passes - 1) {
@@ -56,13 +56,13 @@ __global__ void __launch_bounds__(64) k_time(const uint32_t *keys, uint32_t *sin
     const uint32_t lane = threadIdx.x;
     const size_t g = (size_t)blockIdx.x * 64u + lane;
     uint32_t k[4] = {keys[4 * (g & 4095)], keys[4 * (g & 4095) + 1], keys[4 * (g & 4095) + 2], keys[4 * (g & 4095) + 3]};
-    uint32_t kb[rc4_nkr<NK>::v];
+    uint32_t kb[NK];
     rc4_kb_init<NK>(k, kb);
     uint32_t d[4] = {0, 0, 0, 0};
     for (int x = 0; x < passes; x++) {
         const uint32_t dx = (uint32_t)x ^ (uint32_t)(x - 1);
 #pragma unroll
-        for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+        for (int q = 0; q < NK; q++) kb[q] ^= dx;
         rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
         if (R == 2) {                      /* R2: one KSA + the 4-byte early-reject PRGA per candidate */
             uint32_t jj = 0;
@@ -88,13 +88,13 @@ __global__ void __launch_bounds__(128) k_time2(const uint32_t *keys, uint32_t *s
     const uint32_t lane = threadIdx.x;
     const size_t g = (size_t)blockIdx.x * 64u + lane;
     uint32_t k[4] = {keys[4 * (g & 4095)], keys[4 * (g & 4095) + 1], keys[4 * (g & 4095) + 2], keys[4 * (g & 4095) + 3]};
-    uint32_t kb[rc4_nkr<NK>::v];
+    uint32_t kb[NK];
     rc4_kb_init<NK>(k, kb);
     uint32_t d[4] = {0, 0, 0, 0};
     for (int x = 0; x < passes; x++) {
         const uint32_t dx = (uint32_t)x ^ (uint32_t)(x - 1);
 #pragma unroll
-        for (int q = 0; q < rc4_nkr<NK>::v; q++) kb[q] ^= dx;
+        for (int q = 0; q < NK; q++) kb[q] ^= dx;
         rc4_ksa_asm_kb<NK>(sbase, sbase + (lane << 2), kb);
         if (R == 2) {
             uint32_t jj = 0;

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-dispatch SQ counters of `rc4_ksa_probe time` under rocprofv3 (tools/session_r05k.sh): for each number of
+"""Per-dispatch SQ counters of `rc4_ksa_probe time` under rocprofv3 (tools/sessions/session_r05k.sh): for each number of
 one-wave workgroups per CU, where a chain's wave-cycles go -- parked on s_waitcnt (SQ_WAIT_ANY: the LDS round trips),
 ready but not issued (SQ_WAIT_INST_ANY: another wave holds the issue port) -- and the VALU / LDS instructions issued.
 Usage: tools/rc4_probe_pmc.py gpurun_out/r05k/pmc"""
