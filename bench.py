@@ -309,6 +309,22 @@ def latency_roof(wkey, per_gpu_rate):
             "source": work.RC4_LATENCY_SOURCE}
 
 
+def issue_line(counters, wkey, pwlen):
+    """The VALU issue accounting of the dominant kernel (round 6): the wave-instructions it executes per
+    candidate lane and the SIMD cycles each takes (from the rocprof SQ pass of this build, profiles/pmc_valu.json), the
+    algorithm's minimum instruction count (dprf_amd/work.py INSTR, the same dataflow functions as the slot floor) and
+    their ratio instr_frac = floor / measured.  A kernel at instr_frac ~1 and ~3.9 cycles per instruction sits on the
+    issue cadence of its own instruction mix: only fewer instructions could make it faster."""
+    from dprf_amd import work
+    floor = work.per_candidate(wkey, "instr", part="main", pwlen=pwlen)
+    out = {"instr_floor": floor}
+    if counters and counters.get("valu_instr_per_candidate"):
+        ipc = counters["valu_instr_per_candidate"]
+        out.update(instr_per_candidate=ipc, cycles_per_instr=counters.get("cycles_per_valu_instr"),
+                   instr_frac=floor / ipc, source=counters.get("source"), stale=counters.get("stale"))
+    return out
+
+
 def compact_rocprof(rec):
     return None if not rec else {k: rec[k] for k in ROCPROF_KEYS if rec.get(k) is not None}
 
@@ -337,7 +353,7 @@ def device_balance(ctx):
     return {"devices": devs, "last_over_mean": max(fin) / mean if mean > 0 else None}
 
 
-def summarize(stats, wkey, world, dt):
+def summarize(stats, wkey, world, dt, pwlen=None):
     from dprf_amd import work
     cands = sum(s["candidates"] for s in stats)
     launches = sum(s["launches"] for s in stats)
@@ -347,7 +363,7 @@ def summarize(stats, wkey, world, dt):
     devs = max(1, max(s.get("devices", 1) for s in stats))
     avg_launch_ms = main_ms / max(1, launches)
     per_launch = cands / max(1, launches)
-    floor = work.per_candidate(wkey, part="main")
+    floor = work.per_candidate(wkey, part="main", pwlen=pwlen)
     achieved = per_launch * floor / (avg_launch_ms / 1e3)
     spec = work.per_candidate(wkey, "spec", part="main")
     return {"cands": cands, "launches": launches, "kern_ms": kern_ms, "avg_launch_ms": avg_launch_ms,
@@ -448,7 +464,7 @@ def main():
     dt, stats, lowest, pwlen = run_workload(args.workload, ctx, rank, world, args.steps, args.warmup, sync,
                                             allreduce_min, B, ndev=len(devices), stop_on_first=args.stop_on_first)
     dt_max = allreduce_max(dt)
-    m = summarize(stats, wkey, world, dt_max)
+    m = summarize(stats, wkey, world, dt_max, pwlen)
     peak = work.PEAK_LANE_INSTR_PER_S
     build = _lib.build_id()
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -467,29 +483,35 @@ def main():
             sdt, sst, _, spl = run_workload(name, sctx, rank, world, args.side_steps, 1, sync, allreduce_min,
                                             ndev=len(devices))
             sdt = allreduce_max(sdt)
-            sm = summarize(sst, skey, world, sdt)
+            sm = summarize(sst, skey, world, sdt, spl)
+            per_gpu = sm["value"] / world / max(1, len(devices))
+            pc = pmc_summary(name, build)
             side[name] = {"value": sm["value"], "unit": "candidates/s", "kernel": sctx.kernel, "config": sdesc,
                           "pwlen": spl, "bound": measured_bound(pmc_summary(name, build), skey)[0],
                           "steps": args.side_steps, "avg_launch_ms": sm["kern_ms"] / max(1, sm["launches"]),
                           "dominant_avg_ms": sm["avg_launch_ms"], "candidates_per_launch": sm["per_launch"],
                           # the larger of the launch-time and the wall-time figure: R2-R4 launches overlap on two
                           # streams (a launch's event time then includes its neighbour's), other formats' do not
-                          "valu_floor_frac": max(sm["per_launch"] * work.per_candidate(skey)
+                          "valu_floor_frac": max(sm["per_launch"] * work.per_candidate(skey, pwlen=spl)
                                                  / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak,
-                                                 sm["value"] / world / max(1, len(devices)) * work.per_candidate(skey) / peak),
-                          # SURVEY 8(d)'s spec-level ops per candidate over the same peak, same time base
+                                                 per_gpu * work.per_candidate(skey, pwlen=spl) / peak),
+                          # SURVEY 8(d)'s spec-level VALU ops per candidate over the same peak, same time base; its LDS
+                          # lane-operations against one LDS per CU (round 6: the LDS ops no longer counted as VALU)
                           "spec_frac": max(sm["per_launch"] * work.per_candidate(skey, "spec")
                                            / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3) / peak,
-                                           sm["value"] / world / max(1, len(devices)) * work.per_candidate(skey, "spec") / peak),
+                                           per_gpu * work.per_candidate(skey, "spec") / peak),
+                          "lds_spec_frac": work.lds_spec_frac(skey, per_gpu),
+                          "issue": issue_line(pc, skey, spl),
                           "call_overhead": sm["call_overhead"]}
-            lat = latency_roof(skey, sm["value"] / world / max(1, len(devices)))
+            if skey in work.SPEC_EFFECTIVE:
+                side[name]["spec_effective"] = True
+            lat = latency_roof(skey, per_gpu)
             if lat:
-                side[name]["bound"] = "lds-latency"
+                side[name]["limiter"] = "lds-latency"
                 side[name]["lds_latency"] = lat
             if skey in work.LDS_CYCLES:             # RC4 formats: the modelled LDS-array share (~ rocprof LdsUtil)
                 side[name]["lds_cycle_frac"] = work.lds_frac(
                     skey, sm["per_launch"] / (sm["kern_ms"] / max(1, sm["launches"]) / 1e3))
-            pc = pmc_summary(name, build)
             if pc:
                 side[name]["rocprof"] = compact_rocprof(pc)
             tr, trec = launch_traffic(pmc, name, sm["per_launch"], build)
@@ -521,6 +543,8 @@ def main():
                 "frac": m["achieved"] / peak, "valu_floor_frac": m["achieved"] / peak,
                 # the same kernel time against SURVEY 8(d)'s spec-level op count (2-input ops, 3-input = 2)
                 "spec_frac": m["achieved_spec"] / peak, "spec_achieved": m["achieved_spec"] / 1e12,
+                "lds_spec_frac": work.lds_spec_frac(wkey, m["value"] / world / max(1, len(devices))),
+                "issue": issue_line(counters, wkey, pwlen),
                 "traffic": traffic,
                 "kernel": DOMINANT.get(ctx.kernel, ctx.kernel),
                 "kernel_avg_ms": m["avg_launch_ms"], "candidates_per_launch": m["per_launch"],
@@ -530,11 +554,12 @@ def main():
                 "spec_ops_per_candidate": work.per_candidate(wkey, "spec"),
                 "lds_cycle_frac": work.lds_frac(wkey, m["per_launch"] / (m["avg_launch_ms"] / 1e3)),
                 "call_overhead": m["call_overhead"]}
+        if wkey in work.SPEC_EFFECTIVE:
+            roof["spec_effective"] = True
         lat = latency_roof(wkey, m["value"] / world / max(1, len(devices)))
-        if lat:             # R2-R4: quoted against the chain-latency bound the design can approach (work.py)
+        if lat:             # R2-R4: the chain-latency bound the design can approach (work.py); frac stays the VALU one
             roof["lds_latency"] = lat
-            roof.update(bound="lds-latency", bound_source="model: 9 chains/CU at the unloaded chain latency "
-                        "(tools/rc4_ksa_probe.hip)", frac=lat["frac"])
+            roof["limiter"] = "lds-latency (model: 9 chains/CU at the unloaded chain latency, tools/rc4_ksa_probe.hip)"
         if traffic_rec:
             roof["traffic_source"] = {k: traffic_rec.get(k) for k in ("source", "build", "stale", "fetch_bytes",
                                                                       "write_bytes", "bytes_per_candidate")}
@@ -582,15 +607,25 @@ def main():
             return {"all": round(c["value"], 1), "cores": c.get("cores"), "one": g("one_worker"),
                     "pm4": g("process_model_4")}
 
-        summ = {args.workload: {"value": out["value"], "valu_floor_frac": roof["valu_floor_frac"], "spec_frac": roof["spec_frac"],
-                                "kernel_ms": m["avg_launch_ms"], "cand": int(m["per_launch"]), "steps": args.steps,
-                                "cpu": cpu_short(cpu)}}
+        def issue_short(i):
+            """instructions per candidate, cycles per instruction, instruction floor / measured"""
+            r = lambda x, n: None if x is None else round(x, n)
+            return {"instr_per_candidate": r(i.get("instr_per_candidate"), 1), "cycles_per_instr": r(i.get("cycles_per_instr"), 3),
+                    "instr_frac": r(i.get("instr_frac"), 4)}
+
+        summ = {args.workload: dict({"value": out["value"], "valu_floor_frac": roof["valu_floor_frac"],
+                                     "spec_frac": roof["spec_frac"], "lds_spec_frac": roof["lds_spec_frac"],
+                                     "kernel_ms": m["avg_launch_ms"], "cand": int(m["per_launch"]), "steps": args.steps,
+                                     "cpu": cpu_short(cpu)}, **issue_short(roof["issue"]))}
         if roof.get("lds_latency"):
             summ[args.workload]["lds_latency_frac"] = roof["lds_latency"]["frac"]
         for name, v in side.items():
-            summ[name] = {"value": v["value"], "valu_floor_frac": v["valu_floor_frac"], "spec_frac": v["spec_frac"],
-                          "kernel_ms": v["dominant_avg_ms"], "cand": int(v["candidates_per_launch"]),
-                          "steps": v["steps"], "cpu": cpu_short(side_cpu.get(name))}
+            summ[name] = dict({"value": v["value"], "valu_floor_frac": v["valu_floor_frac"], "spec_frac": v["spec_frac"],
+                               "lds_spec_frac": v["lds_spec_frac"], "kernel_ms": v["dominant_avg_ms"],
+                               "cand": int(v["candidates_per_launch"]), "steps": v["steps"],
+                               "cpu": cpu_short(side_cpu.get(name))}, **issue_short(v["issue"]))
+            if v.get("spec_effective"):
+                summ[name]["spec_effective"] = True
             if v.get("lds_latency"):
                 summ[name]["lds_latency_frac"] = v["lds_latency"]["frac"]
         if cluster and cluster.get("value") is not None:

@@ -10,7 +10,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 ALL_DEVICES = -1
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
@@ -32,16 +32,17 @@ class DprfError(RuntimeError):
 class Stats(ctypes.Structure):
     _fields_ = [("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("wall_ms", ctypes.c_double), ("stopped_early", ctypes.c_uint32), ("devices", ctypes.c_uint32),
-                ("main_kernel_ms", ctypes.c_double)]
+                ("main_kernel_ms", ctypes.c_double), ("hit_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class DeviceStats(ctypes.Structure):
-    """dprf_device_stats (ABI 4): one device's share of the last call on a context."""
+    """dprf_device_stats (ABI 4; `evaluated` ABI 6): one device's share of the last call on a context."""
     _fields_ = [("device", ctypes.c_int32), ("launches", ctypes.c_uint32), ("candidates", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double), ("first_ms", ctypes.c_double), ("finish_ms", ctypes.c_double)]
+                ("kernel_ms", ctypes.c_double), ("first_ms", ctypes.c_double), ("finish_ms", ctypes.c_double),
+                ("evaluated", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -14,6 +14,7 @@
 #include "dev_crypto.h"
 #include "dprf_params.h"
 #include "dprf_launch.h"
+#include "dprf_hits.h"
 #include "rc4_dev.h"
 
 /* ------------------------------------------------------------------ candidate source */
@@ -71,7 +72,7 @@ DEVI void get_candidate(const dprf_enum &e, const uint8_t *cs, uint32_t g, cand 
 /* ------------------------------------------------------------------ block prologue / epilogue */
 /* Stage the charset (and optionally the AES tables) into LDS and decide once per block whether it runs.
  * With stop_on_first a block is skipped only when its LOWEST candidate index lies above the lowest hit
- * found so far (R->first): every index below the final `first` is then verified whatever order the
+ * known so far (R->first, and across devices the call's, dprf_hits.h): every index below the final `first` is then verified whatever order the
  * workgroups are dispatched in, so the reported hit is the lowest of the call unconditionally (a boolean
  * stop flag would let a late-dispatched lower block skip itself).  `per` = candidates per thread.
  * COUNT: this kernel's skipped blocks are counted in R->skipped (the verifying kernel of a format; the
@@ -93,7 +94,7 @@ DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_resu
         uint32_t skip = 0u;
         if (stop_on_first) {
             const uint32_t off = blockIdx.x * blockDim.x * per;
-            skip = e.start + off > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+            skip = e.start + off > lowest_known(e, R) ? 1u : 0u;
             if (skip && COUNT) {
                 const uint32_t n = e.count - off < blockDim.x * per ? e.count - off : blockDim.x * per;
                 atomicAdd(&R->skipped, (unsigned long long)n);
@@ -105,12 +106,6 @@ DEVI bool block_prologue(const dprf_enum &e, const dprf_aes_tables *T, dprf_resu
     return *flag == 0;
 }
 
-DEVI void report_hit(dprf_results *R, unsigned long long idx, uint32_t cap, uint32_t stop_on_first) {
-    uint32_t slot = atomicAdd(&R->nhits, 1u);
-    if (slot < cap) R->hits[slot] = idx;
-    atomicMin(&R->first, idx);
-    if (stop_on_first) atomicExch(&R->stop, 1u);
-}
 
 /* BE message words of `len` candidate bytes (LE-packed) placed after `pre` bytes already in m[],
  * pre a multiple of 4 and <= 16, with the 0x80 terminator.  Static indices only.  A candidate that fills its whole
@@ -217,7 +212,7 @@ k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, 
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < 8; k++) ok = ok && h[k] == lp.target[k];
-        if (ok) report_hit(R, rec, cap, stop_on_first);
+        if (ok) report_hit(e, R, rec, cap, stop_on_first);
         return;
     }
 #pragma unroll
@@ -320,7 +315,7 @@ k_office_check(dprf_enum e, dprf_office_params p, const dprf_aes_tables *T, dprf
         sha1_compress(vh, w);
     }
     ok = ok && vh[0] == dh0[0] && vh[1] == dh0[1] && vh[2] == dh0[2] && vh[3] == dh0[3] && vh[4] == dh1[0];
-    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+    if (valid && ok) report_hit(e, R, e.start + g, cap, stop_on_first);
 }
 
 #endif /* DPRF_PART_OFFICE */
@@ -568,7 +563,7 @@ k_odt_check(dprf_enum e, dprf_odt_params p, const dprf_aes_tables *T, dprf_resul
 #pragma unroll
         for (int k = 0; k < 8; k++) ok = ok && st[k] == p.checksum[k];
     }
-    if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+    if (valid && ok) report_hit(e, R, e.start + g, cap, stop_on_first);
 #undef ODT_DECRYPT
 }
 #endif /* DPRF_PART_ODT */
@@ -694,7 +689,7 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
                 b[j] = j < NW ? (lo ? w0[j] : w1[j]) : tail[j];
                 if (j < NW && (uint32_t)j == lw) b[j] |= ch;
             }
-            if (sha256_block_matches(b, p.u, valid)) report_hit(R, e.start + g, cap, stop_on_first);
+            if (sha256_block_matches(b, p.u, valid)) report_hit(e, R, e.start + g, cap, stop_on_first);
         }
         return;
     }
@@ -711,7 +706,7 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
             uint32_t b[16];
 #pragma unroll
             for (int j = 0; j < 16; j++) b[j] = (j < NW ? bswap32(c.w[j]) : 0u) | tail[j];
-            if (sha256_block_matches(b, p.u, valid)) report_hit(R, e.start + g, cap, stop_on_first);
+            if (sha256_block_matches(b, p.u, valid)) report_hit(e, R, e.start + g, cap, stop_on_first);
             continue;
         }
         /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
@@ -738,7 +733,7 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
         bool ok = true;
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) ok = ok && hh[kk] == p.u[kk];
-        if (valid && ok) report_hit(R, e.start + g, cap, stop_on_first);
+        if (valid && ok) report_hit(e, R, e.start + g, cap, stop_on_first);
     }
 }
 
@@ -969,7 +964,7 @@ k_pdf_r24(dprf_enum e, dprf_pdf_params p, dprf_results *R_, uint32_t cap, uint32
                 if (!__builtin_amdgcn_ballot_w64(valid && pre)) break;
             }
         }
-        if (valid && ok) report_hit(R_, e.start + g, cap, stop_on_first);
+        if (valid && ok) report_hit(e, R_, e.start + g, cap, stop_on_first);
     }
 }
 

@@ -26,6 +26,7 @@
 #include "dev_crypto.h"
 #include "dprf_params.h"
 #include "dprf_launch.h"
+#include "dprf_hits.h"
 
 #include <mutex>
 
@@ -750,7 +751,7 @@ DEVI bool r6_start(const dprf_enum &e, const dprf_pdf_params &p, const uint8_t *
      * reported hit the lowest of the call */
     if (c >= lds_load(&sh->ncand)) {
         c = R6_IDLE;
-    } else if (stop_on_first && lds_load64(&sh->start) + c > __hip_atomic_load(&R->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    } else if (stop_on_first && lds_load64(&sh->start) + c > lowest_known(e, R)) {
         atomicAdd(&R->skipped, 1ull);
         c = R6_IDLE;
     }
@@ -911,13 +912,7 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
                 bool ok = true;
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) ok = ok && K[kk] == p.u[kk];
-                if (ok) {
-                    const unsigned long long idx = lds_load64(&sh->start) + sh->cand[slot];
-                    uint32_t h = atomicAdd(&R->nhits, 1u);
-                    if (h < cap) R->hits[h] = idx;
-                    atomicMin(&R->first, idx);
-                    if (stop_on_first) atomicExch(&R->stop, 1u);
-                }
+                if (ok) report_hit(e, R, lds_load64(&sh->start) + sh->cand[slot], cap, stop_on_first);
                 /* the finishing lanes of the batch take their next candidates together */
                 more = r6_start<MODE>(e, p, cs, R, stop_on_first, sh, S, slot, r6_take(R, true, opaque_lane()));
                 if (!more) atomicSub(&sh->live, 1u);

@@ -31,6 +31,9 @@ struct dprf_enum {
     const uint64_t *loff;           /* long list: [n] word offset of each record in the blob (16-byte aligned)    */
     const uint32_t *llen;           /* long list: [n] byte length of each record                                  */
     uint32_t *keys;                 /* long list: [8][count] prehash output (chunk-local), read by the next kernel */
+    /* multi-device stop_on_first calls only (round 6, dprf_hits.h), else null: host-mapped words */
+    unsigned long long *hit_mirror;         /* this device lane's lowest hit, lowered by its kernels             */
+    const unsigned long long *xfirst;       /* the lowest hit any device of the call has reported (host-kept)    */
 };
 
 /* Long-list prehash (k_long_prehash): the first message of the format's verify() over a record of any length. */

@@ -19,9 +19,23 @@ Floor.  The per-candidate work is the fewest issue slots the ALGORITHM needs on 
 table, derived per primitive from its dataflow (sha1_floor() below does it exactly from which message
 words are constant); a kernel that spends more slots than the floor shows a lower fraction of peak.
 
-The survey's own per-unit figures (SURVEY.md 8(d), 2-input spec ops, 3-input op = 2) are kept in SPEC for
-reference.
+The survey's own per-unit figures (SURVEY.md 8(d), 2-input spec ops, 3-input op = 2) are SPEC, split (round 6,
+VERDICT r5 #2) into the VALU ops the SIMDs issue (SPEC) and the LDS lane-operations of the table lookups (SPEC_LDS:
+AES 160 / 224 per block, RC4 1,024 per KSA and 5 per PRGA byte), which the LDS executes, not the VALU: spec_frac
+counts VALU ops only against the VALU peak, lds_spec_frac the LDS ops against one LDS per CU (32 lane-operations per
+LDS-array cycle when conflict-free, MI355X_MICROARCH.md).
+
+Instruction floor (round 6).  What bounds every VALU kernel here is its wave-instruction COUNT: the counters show
+all of them issuing at ~3.9 cycles per wave-instruction (the mixed half/full-rate cadence of these streams,
+profiles/valu_occ_r05t.txt), so the headroom is measured instructions per candidate against the fewest the algorithm
+needs.  INSTR is that minimum per primitive in wave-instructions per lane, from the same dataflow functions as the
+slot floor with unit "instr": every VALU instruction counts 1; three-input forms are used where gfx950 has them
+(v_add3_u32 for a sum of three, v_bitop3_b32 for any 3-input bitwise function, v_lshl_add_u64 for a 64-bit add);
+a rotate is one v_alignbit (a 64-bit rotate two); a table lookup's address one v_perm of the state byte and the
+lane's table base (the split-table AES of the R6 and ODF kernels).  bench.py divides it by SQ_INSTS_VALU x 64 /
+candidates of the profiled dispatch (instr_frac).
 """
+import math
 
 PEAK_SLOTS_PER_S = 256 * 4 * 32 * 2.4e9   # 78.64e12 full-rate VALU lane-slots/s
 PEAK_LANE_INSTR_PER_S = PEAK_SLOTS_PER_S   # backwards-compatible name
@@ -31,11 +45,22 @@ COST = {"add": 1.0, "xor": 1.0, "and": 1.0, "or": 1.0, "shr": 1.0, "shl": 2.0, "
         "add3": 2.0, "perm": 2.0, "bfe": 2.0}
 
 
-def sha1_floor(const_words, uniform_words=()):
+def _nadd(terms, unit):
+    """a sum of `terms` values: terms - 1 additions, or (unit "instr") ceil((terms - 1) / 2) v_add3"""
+    if terms <= 1:
+        return 0
+    return math.ceil((terms - 1) / 2) if unit == "instr" else (terms - 1) * COST["add"]
+
+
+def sha1_floor(const_words, uniform_words=(), unit="slots"):
     """Issue-slot floor of one SHA-1 compression whose message words `const_words` are compile-time
     constants and `uniform_words` are wave-uniform (scalar unit, free for the VALU).  The chaining value
     is variable.  Per round: rol5 + f + (terms-1) additions + rol30; per schedule word: the XOR of its
-    non-constant inputs + rol1."""
+    non-constant inputs + rol1.  unit "instr": wave-instructions instead (module docstring)."""
+    ins_cost = {"slots": {1: 0, 2: COST["xor"], 3: COST["bitop3"], 4: COST["bitop3"] + COST["xor"]},
+                "instr": {1: 0, 2: 1, 3: 1, 4: 2}}[unit]
+    rot = COST["rot"] if unit == "slots" else 1
+    f_ = COST["bitop3"] if unit == "slots" else 1
     kind = ["v"] * 16
     for i in const_words:
         kind[i] = "c"
@@ -50,18 +75,21 @@ def sha1_floor(const_words, uniform_words=()):
             if nv == 0:
                 wt = "u" if "u" in ins else "c"
             else:
-                slots += {1: 0, 2: COST["xor"], 3: COST["bitop3"], 4: COST["bitop3"] + COST["xor"]}[nv] + COST["rot"]
+                slots += ins_cost[nv] + rot
                 wt = "v"
             w.append(wt)
         wt = w[t]
-        # a' = rol5(a) + f(b,c,d) + e + (K + W): K+W folds when W is not a VGPR value
-        terms = 3 + (1 if wt == "v" else 0) + (1 if wt != "v" else 0)   # rol5, f, e, W, [K(+W)]
+        # a' = rol5(a) + f(b,c,d) + e + K + W: K+W folds when W is not a VGPR value (rol5, f, e, [K+W] or K, W)
         terms = 4 if wt != "v" else 5
-        slots += COST["rot"] + COST["bitop3"] + (terms - 1) * COST["add"] + COST["rot"]
-    return slots + 5 * COST["add"]
+        slots += rot + f_ + _nadd(terms, unit) + rot
+    return slots + 5 * (COST["add"] if unit == "slots" else 1)
 
 
-def sha256_floor():
+def sha256_floor(unit="slots"):
+    if unit == "instr":
+        # Sigma1 (3 rotates + xor3) + Ch + t1 = h + S1 + Ch + K + W (2 add3) + Sigma0 + Maj + a' = t1 + S0 + Maj
+        # (add3) + e' = d + t1; schedule: sigma0 / sigma1 (2 rotates + shift + xor3 each) + W (2 add3)
+        return 64 * (4 + 1 + 2 + 4 + 1 + 1 + 1) + 48 * (4 + 4 + 2) + 8
     rnd = 3 * COST["rot"] + COST["bitop3"] + COST["bitop3"] + 4 * COST["add"] + 3 * COST["rot"] + COST["bitop3"] \
         + COST["bitop3"] + 2 * COST["add"] + COST["add"]
     sched = 2 * (2 * COST["rot"] + COST["shr"] + COST["bitop3"]) + 3 * COST["add"]
@@ -78,6 +106,8 @@ def sha256_dataflow(var_words, rounds=64, unit="floor"):
     With rounds < 64 the final additions are the one compare word's (k_pdf_r5's early reject after round 60)."""
     if unit == "spec":
         big_s, ch, maj, small_s, add = 5, 4, 5, 5, 1
+    elif unit == "instr":
+        big_s, ch, maj, small_s, add = 4, 1, 1, 4, 1
     else:
         big_s = 3 * COST["rot"] + COST["bitop3"]
         ch = maj = COST["bitop3"]
@@ -85,7 +115,10 @@ def sha256_dataflow(var_words, rounds=64, unit="floor"):
         add = COST["add"]
 
     def adds(n_var, n_other):
-        return 0 if n_var == 0 else (n_var - 1 + (1 if n_other else 0)) * add
+        if n_var == 0:
+            return 0
+        terms = n_var + (1 if n_other else 0)
+        return math.ceil((terms - 1) / 2) if unit == "instr" else (terms - 1) * add
 
     w = [i in var_words for i in range(16)]
     work = 0.0
@@ -99,22 +132,32 @@ def sha256_dataflow(var_words, rounds=64, unit="floor"):
         work += (big_s if e else 0) + (ch if (e or f or g) else 0) + adds(sum(t1_var), 1)
         t1 = any(t1_var)
         t2 = a or b or c
-        work += (big_s if a else 0) + (maj if t2 else 0) + (add if a and t2 else 0)
+        work += (big_s if a else 0) + (maj if t2 else 0)
+        if unit == "instr":                        # a' = t1 + S0 + Maj in one v_add3 (or one add / none)
+            work += 1 if (t1 or t2) else 0
+        else:
+            work += (add if a and t2 else 0) + (add if (t1 or t2) else 0)   # t2 = S0 + Maj, a' = t1 + t2
         work += add if (d or t1) else 0            # e' = d + t1
-        work += add if (t1 or t2) else 0           # a' = t1 + t2
         h, g, f, e, d, c, b, a = g, f, e, (d or t1), c, b, a, (t1 or t2)
     return work + (8 if rounds == 64 else 1) * add
 
 
-def sha512_floor():
+def sha512_floor(unit="slots"):
+    if unit == "instr":
+        # 64-bit values as register pairs: a rotate 2 v_alignbit, a shift 2, a 3-input bitwise op 2 v_bitop3, an add one
+        # v_lshl_add_u64.  Round: S1 8 + Ch 2 + t1 (4 adds) + S0 8 + Maj 2 + a' (2 adds) + e' 1; schedule: s0, s1 8 each
+        # + 3 adds
+        return 80 * (8 + 2 + 4 + 8 + 2 + 2 + 1) + 64 * (8 + 8 + 3) + 8
     add64, rot64, shr64, x64 = 2 * COST["add"], 2 * COST["rot"], COST["rot"] + COST["shr"], 2 * COST["bitop3"]
     rnd = (3 * rot64 + x64) + x64 + 4 * add64 + (3 * rot64 + x64) + x64 + 2 * add64 + add64
     sched = 2 * (2 * rot64 + shr64 + x64) + 3 * add64
     return 80 * rnd + 64 * sched + 8 * add64
 
 
-def md5_floor(n_const_words=0):
+def md5_floor(n_const_words=0, unit="slots"):
     # F/G/H/I as one bitop3, a + f + (K + M) (K+M folds for constant M), rotate, + b
+    if unit == "instr":   # a + f + K + M: 2 instructions (one v_add3 when K + M is one constant), rotate, + b
+        return 64 * (1 + 2 + 1 + 1) - n_const_words * 4
     var = 64 * (COST["bitop3"] + 3 * COST["add"] + COST["rot"] + COST["add"])
     return var - n_const_words * 4 * COST["add"]
 
@@ -141,17 +184,48 @@ FLOOR = {
     "rc4_ksa": 256 * (2 * COST["add"] + COST["and"] + COST["shl"] + COST["or"]) + 64 * COST["add"],
     "rc4_prga_byte": 2 * COST["add"] + 2 * (COST["and"] + COST["shl"] + COST["or"]) + COST["shl"] + COST["xor"],
 }
+# The instruction floor per primitive (module docstring).  AES with split T-tables in LDS: one v_perm address per
+# lookup, two v_bitop3 (XOR3) per output column of a round; the last round's 16 S-box bytes assembled by 3 v_perm per
+# word + the key XOR; the initial AddRoundKey 4 XOR; CBC 4 XOR.  Key schedules: 4 S-box addresses + 3 v_perm + 5 XOR
+# per AES-128 round key (AES-256: 8 words per two round keys); the decryption schedule's InvMixColumns by 4 lookups
+# + 2 XOR3 per word.  RC4: per KSA step j += S[i] + K (v_add3) and the S[j] address (2: the [i/4][lane][i%4] layout);
+# the identity's 63 adds; per PRGA byte j += S[i], two addresses, the output lookup's address and the XOR.
+AES_ROUND_I = 16 + 8
+AES_LAST_I = 16 + 4 * (3 + 1)
+INSTR = {
+    "sha1c": sha1_floor((), unit="instr"),
+    "sha1c_office_loop": sha1_floor(range(6, 16), (0,), unit="instr"),
+    "sha1c_hmac20": sha1_floor(range(5, 16), unit="instr"),
+    "sha256c": sha256_floor("instr"), "sha512c": sha512_floor("instr"), "md5c": md5_floor(0, "instr"),
+    "md5c_16": md5_floor(12, "instr"), "md5c_5": md5_floor(14, "instr"),
+    "aes128_enc_block": 9 * AES_ROUND_I + AES_LAST_I + 4 + 4,
+    "aes128_dec_block": 9 * AES_ROUND_I + AES_LAST_I + 4,
+    "aes256_dec_block": 13 * AES_ROUND_I + AES_LAST_I + 4 + 4,
+    "aes128_keyexp": 10 * (4 + 3 + 5),
+    "aes128_dec_sched": 9 * 4 * (4 + 2),
+    "aes256_keyexp_dec_sched": 7 * (8 + 6 + 9) + 13 * 4 * (4 + 2),
+    "rc4_ksa": 256 * (1 + 2) + 63,
+    "rc4_prga_byte": 1 + 2 + 1 + 2 + 1,
+}
 # PDF R5 at its bench configuration (-pr 7: message words 0-1 carry the candidate, 2-15 are launch-uniform salt,
 # padding and length; the compare of IV7 + e after round 60 rejects all but 2^-32 of the candidates): the dataflow
 # floor of the early-reject compression (1,925 slots, against 2,200 for a compression of 16 per-lane words).
 FLOOR["sha256c_r5"] = sha256_dataflow({0, 1}, rounds=61)
+INSTR["sha256c_r5"] = sha256_dataflow({0, 1}, rounds=61, unit="instr")
 # the floor a format's kernel is held to where its primitive runs on fewer per-lane inputs than the generic one
 FLOOR_AS = {"pdf_r5": {"sha256c": "sha256c_r5"}}
-SPEC = {
+SPEC = {   # SURVEY.md 8(d), VALU ops only (its AES / RC4 figures less their LDS ops, SPEC_LDS)
     "sha1c": 1001, "sha1c_office_loop": 1001, "sha1c_hmac20": 1001, "sha256c": 2296, "sha512c": 5840,
-    "md5c": 532, "md5c_16": 532, "md5c_5": 532, "aes128_enc_block": 640, "aes128_dec_block": 640, "aes256_dec_block": 896,
-    "aes128_keyexp": 0, "aes128_dec_sched": 0, "aes256_keyexp_dec_sched": 0, "rc4_ksa": 2304, "rc4_prga_byte": 16,
+    "md5c": 532, "md5c_16": 532, "md5c_5": 532, "aes128_enc_block": 480, "aes128_dec_block": 480, "aes256_dec_block": 672,
+    "aes128_keyexp": 0, "aes128_dec_sched": 0, "aes256_keyexp_dec_sched": 0, "rc4_ksa": 1280, "rc4_prga_byte": 11,
 }
+SPEC_LDS = {"aes128_enc_block": 160, "aes128_dec_block": 160, "aes256_dec_block": 224, "rc4_ksa": 1024,
+            "rc4_prga_byte": 5}   # LDS lane-operations per unit
+LDS_LANE_OPS_PER_CYCLE = 32       # one conflict-free LDS access of 32 lanes per LDS-array cycle (a wave64 op: 2)
+# Formats whose spec count includes work the kernel by design does not execute (R5: rounds 61-63 after the early
+# reject, and the launch-uniform message words on the scalar unit): their spec_frac is an EFFECTIVE rate, not a
+# fraction of issued work.
+SPEC_EFFECTIVE = {"pdf_r5"}
 
 # Exact primitive counts per candidate (cross-checked against oracle.work_counts in
 # tests/test_work_accounting.py).
@@ -236,10 +310,26 @@ def lds_frac(fmt, cand_per_s):
     return cand_per_s * LDS_CYCLES[fmt] / PEAK_LDS_CYCLES_PER_S
 
 
-def per_candidate(fmt, unit="floor", part="all"):
-    """Issue slots (unit "floor") or survey spec ops (unit "spec") per candidate; part "main" counts only
-    the dominant kernel's share (MAIN)."""
-    table = FLOOR if unit == "floor" else SPEC
+def r5_floor(pwlen, unit="floor"):
+    """PDF R5's early-reject compression for range candidates of `pwlen` bytes: the message words holding password
+    bytes vary per lane (a word shared with the salt too), the rest are launch-uniform (the -pr 7 figure,
+    words 0-1, is right for -pr 5..8 only)"""
+    return sha256_dataflow(set(range(max(1, math.ceil(pwlen / 4)))), 61, "instr" if unit == "instr" else "floor")
+
+
+def per_candidate(fmt, unit="floor", part="all", pwlen=None):
+    """Per candidate: issue slots (unit "floor"), wave-instructions (unit "instr": the instruction floor), the survey's
+    VALU spec ops (unit "spec") or its LDS lane-operations (unit "spec_lds"); part "main" counts only the dominant
+    kernel's share (MAIN).  pwlen: the range length the floor of PDF R5 depends on (default: its bench's 7)."""
+    table = {"floor": FLOOR, "instr": INSTR, "spec": SPEC, "spec_lds": SPEC_LDS}[unit]
     counts = MAIN.get(fmt, COUNTS[fmt]) if part == "main" else COUNTS[fmt]
-    alias = FLOOR_AS.get(fmt, {}) if unit == "floor" else {}
-    return sum(table[alias.get(k, k)] * v for k, v in counts.items())
+    if fmt == "pdf_r5" and pwlen is not None and unit in ("floor", "instr"):
+        return r5_floor(pwlen, unit) * counts["sha256c"]
+    alias = FLOOR_AS.get(fmt, {}) if unit in ("floor", "instr") else {}
+    return sum(table.get(alias.get(k, k), 0) * v for k, v in counts.items())
+
+
+def lds_spec_frac(fmt, cand_per_s, part="all", cus=256, clock=2.4e9):
+    """Fraction of the chip's LDS-array cycles (one LDS per CU) the survey's LDS lane-operations of `cand_per_s`
+    candidates take (0 for formats without table lookups)."""
+    return cand_per_s * per_candidate(fmt, "spec_lds", part) / LDS_LANE_OPS_PER_CYCLE / (cus * clock)

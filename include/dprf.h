@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 5
+#define DPRF_ABI_VERSION 6
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -87,6 +87,8 @@ typedef struct dprf_stats {
     uint32_t devices;      /* devices that took part in the call (ABI 3; was `reserved`)        */
     double main_kernel_ms; /* HIP-event time of the dominant kernel alone: the KDF kernel for Office/ODF
                               (their check kernel follows it on the same stream), else = kernel_ms  (ABI 2) */
+    double hit_ms;         /* host time from the call's start to when the library first knew of a hit, -1 if none
+                              (ABI 6): wall_ms - hit_ms is how long the call ran on after its answer existed */
 } dprf_stats;
 /* kernel_ms / main_kernel_ms are summed over the devices of a multi-device call (device time); wall_ms is
  * the call's wall time.  candidates / launches are totals over the devices.  PDF R2-R4 alternate consecutive
@@ -103,6 +105,7 @@ typedef struct dprf_device_stats {
     double kernel_ms;      /* HIP-event device time of its launches                                    */
     double first_ms;       /* host time from the call's start to its first launch                      */
     double finish_ms;      /* host time from the call's start to when its last launch was retired      */
+    uint64_t evaluated;    /* candidates it verified: `candidates` minus the stop_on_first skips (ABI 6) */
 } dprf_device_stats;
 
 /* ---- library ---- */
@@ -152,14 +155,19 @@ int dprf_ctx_last_call_devices(const dprf_ctx *ctx, dprf_device_stats *out, int 
  * character most significant).  The symbols are the charset's BYTES, all distinct (a repeated byte would
  * verify candidates twice: DPRF_E_CHARSET): for PDF and ODF a byte >= 0x80 is a raw candidate byte, as the
  * reference's argv carries it; Office takes ASCII only.  A caller whose alphabet has multi-byte UTF-8
- * characters spells the window itself and verifies it with dprf_verify_list (brute_force.search_round).  Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total
- * number of hits found (may exceed cap).  stats may be NULL.
+ * characters spells the window itself and verifies it with dprf_verify_list (brute_force.search_round).
+ * Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total number of hits found (may exceed cap).
+ * stats may be NULL.
  * Multi-device: the devices take contiguous chunks of the range from one shared cursor in increasing
  * order (chunks sized for ~0.1-1 s of device time at the rate measured on that device), so a fast device
  * takes more and every index below the last chunk taken is covered.
  * stop_on_first != 0: the search ends once no unverified index lies below the lowest hit found so far;
  * hits[0] is then the LOWEST verifying index of the whole range, unconditionally (every candidate below
- * it is verified on some device; a kernel block is skipped only if its lowest index is above it). */
+ * it is verified on some device; a kernel block is skipped only if its lowest index is above it).  A
+ * multi-device call pushes a hit to the launches already running on the other devices (ABI 6): a host thread
+ * polls every lane's host-mapped hit word and publishes the minimum to a word every launch reads beside its own
+ * device's (dprf_hits.h), so their blocks above it skip within ~0.2 ms -- as the reference's workers stop at
+ * their next candidate once `found` is set (brute_force.py:111-114, :140-147).  The same holds in list mode. */
 int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwlen, uint64_t start,
                       uint64_t count, int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits,
                       dprf_stats *stats);

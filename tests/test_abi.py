@@ -69,3 +69,27 @@ def test_makefile_tracks_every_local_header():
                 if inc == "build_id.h":
                     continue                      # generated into OBJDIR by the Makefile itself
                 assert inc in hdrs, (f, inc)
+
+
+def test_ctypes_structs_match_the_header_layout(tmp_path):
+    """dprf_stats / dprf_device_stats as a C compiler lays them out (include/dprf.h) == the ctypes mirrors (ABI 6
+    appended hit_ms and evaluated): sizes and every field offset."""
+    import subprocess
+    from dprf_amd import _lib
+    src = tmp_path / "layout.c"
+    fields = {"dprf_stats": [f for f, _ in _lib.Stats._fields_],
+              "dprf_device_stats": [f for f, _ in _lib.DeviceStats._fields_]}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dprf.h"', "int main(void) {"]
+    for t, fs in fields.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (t, t))
+        for f in fs:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (t, f, t, f))
+    lines.append("return 0; }")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if ln)
+    for t, cls in (("dprf_stats", _lib.Stats), ("dprf_device_stats", _lib.DeviceStats)):
+        assert int(got[t]) == ctypes.sizeof(cls), t
+        for f, _ in cls._fields_:
+            assert int(got["%s.%s" % (t, f)]) == getattr(cls, f).offset, (t, f)

@@ -142,3 +142,45 @@ def test_sha256_dataflow_floor():
     assert work.per_candidate("pdf_r5", "spec") == 2296
     # uniform words only remove work, never add it
     assert work.sha256_dataflow({0}, 61) <= r5 <= work.sha256_dataflow(set(range(8)), 61)
+
+
+def test_spec_split_and_instruction_floor():
+    """Round 6: SURVEY 8(d)'s per-unit figures split into VALU ops (spec_frac) and LDS lane-operations
+    (lds_spec_frac: 32 per LDS-array cycle, one LDS per CU); the instruction floor per primitive; PDF R5's floor by
+    the range length."""
+    import math
+    assert work.SPEC["aes128_enc_block"] + work.SPEC_LDS["aes128_enc_block"] == 640
+    assert work.SPEC["aes256_dec_block"] + work.SPEC_LDS["aes256_dec_block"] == 896
+    assert work.SPEC["rc4_ksa"] + work.SPEC_LDS["rc4_ksa"] == 2304
+    assert work.SPEC["rc4_prga_byte"] + work.SPEC_LDS["rc4_prga_byte"] == 16
+    # R6's VALU-only spec ops per candidate: 17.72 M (the verdict's recomputation)
+    assert abs(work.per_candidate("pdf_r6", "spec") - 17.72e6) / 17.72e6 < 0.001
+    assert work.per_candidate("odt", "spec_lds", "main") == 0 and work.per_candidate("office", "spec_lds") == 3 * 160
+    assert abs(work.lds_spec_frac("pdf_r34", 6.26e8) - 6.26e8 * 22080 / 32 / (256 * 2.4e9)) < 1e-12
+    # instruction floors: SHA-1 5 per round + its schedule; the PBKDF2 compression (20-byte message) 578
+    assert work.INSTR["sha1c_hmac20"] == 578 and work.INSTR["sha1c"] == 597
+    assert work.INSTR["sha256c"] == 64 * 14 + 48 * 10 + 8 and work.INSTR["sha512c"] == 80 * 27 + 64 * 19 + 8
+    assert round(work.per_candidate("odt", "instr", "main")) == 4094 * 578 + 4 * 597 + 1384
+    for fmt in work.COUNTS:
+        assert work.per_candidate(fmt, "instr", "main") < work.per_candidate(fmt, "floor", "main"), fmt
+    # R5: the -pr 7 figure is the 2-word one; longer ranges hold more per-lane words and a higher floor
+    assert work.per_candidate("pdf_r5", pwlen=7) == work.per_candidate("pdf_r5") == work.FLOOR["sha256c_r5"]
+    assert work.per_candidate("pdf_r5", pwlen=5) == work.per_candidate("pdf_r5", pwlen=8)
+    assert work.per_candidate("pdf_r5", pwlen=9) > work.per_candidate("pdf_r5", pwlen=8)
+    assert work.r5_floor(32) == work.sha256_dataflow(set(range(8)), 61)
+    assert work.per_candidate("pdf_r5", "instr", pwlen=7) == work.INSTR["sha256c_r5"] == math.floor(
+        work.sha256_dataflow({0, 1}, 61, "instr"))
+
+
+def test_issue_line_from_a_profile():
+    """bench.issue_line: measured instructions per candidate and cycles per instruction from the PMC record, the floor
+    from work.INSTR, instr_frac their ratio; without a record only the floor."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    rec = {"valu_instr_per_candidate": 2370181.0, "cycles_per_valu_instr": 3.936, "source": "x", "stale": False}
+    i = bench.issue_line(rec, "odt", 6)
+    assert i["instr_floor"] == work.per_candidate("odt", "instr", "main")
+    assert abs(i["instr_frac"] - i["instr_floor"] / 2370181.0) < 1e-12 and i["cycles_per_instr"] == 3.936
+    assert bench.issue_line(None, "pdf_r6", 6) == {"instr_floor": work.per_candidate("pdf_r6", "instr", "main")}

@@ -13,7 +13,8 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CUS, XCDS = 256, 8
+CUS, XCDS, SIMDS = 256, 8, 1024
+PMC_STEPS = 2          # tools/profile_gpu.sh counts two steps of bench.py per PMC pass (prof_summary.py)
 DOM = {"odt": "k_odt_kdf", "odt_e": "k_odt_kdf", "office": "k_office_kdf", "pdf_r34": "k_pdf_r24",
        "pdf_r3": "k_pdf_r24", "pdf_r3_40": "k_pdf_r24", "pdf_r2": "k_pdf_r24", "pdf_r5": "k_pdf_r5",
        "pdf_r6": "k_pdf_r6"}
@@ -40,7 +41,17 @@ for w, kname in DOM.items():
                           "fetch_bytes": pd.get("FETCH_SIZE", 0) * 1024, "write_bytes": pd.get("WRITE_SIZE", 0) * 1024,
                           "source": src, "build": build}
         if v.get("valu_busy") is not None:
+            # the issue line (round 6): wave-instructions per candidate lane over the counted steps'
+            # dispatches (bench.py --steps 2: 2 x batch candidates), and SIMD cycles per wave-instruction within the
+            # SQ pass (GRBM_GUI_ACTIVE / XCDs = the dispatch's cycles on every CU)
+            batch = ((d.get("bench_under_profiler") or {}).get("config") or {}).get("batch_per_gpu")
+            tot = v.get("per_run_total", {})
+            sq = v.get("passes", {}).get("sq", {})
+            ipc = tot["SQ_INSTS_VALU"] * 64 / (batch * PMC_STEPS) if batch and tot.get("SQ_INSTS_VALU") else None
+            cpi = (sq["GRBM_GUI_ACTIVE"] / XCDS * SIMDS / sq["SQ_INSTS_VALU"]
+                   if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") else None)
             valu[w] = {"kernel": k, "valu_busy": v.get("valu_busy"), "valu_utilization": v.get("valu_utilization"),
+                       "valu_instr_per_candidate": ipc, "cycles_per_valu_instr": cpi,
                        "lds_busy": v.get("lds_busy"), "lds_util": v.get("lds_util"),
                        "effective_clock_GHz": v.get("effective_clock_GHz"),
                        "valu_active_per_wave_cycle": v.get("valu_active_per_wave_cycle"),
