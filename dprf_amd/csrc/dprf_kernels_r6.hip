@@ -14,14 +14,12 @@
  *    its own LDS bank column ([word][lane], so a lane's words share one bank) and pulls each 16-byte
  *    block out of it with 5 ds_read_b32 + 4 v_perm; ciphertext goes straight into the SHA message
  *    registers 64 bytes (4 AES blocks) at a time.
- *  - AES T-tables: Te0 and Te2 = ror16(Te0), each replicated 32x across banks (lane l reads copy l%32);
- *    a round column is Te0[a] ^ Te2[c] ^ ror8(Te0[b] ^ Te2[d] ^ rol8 k), one rotate instead of three.
- *    The last round takes S[x] from byte 2 of Te0[x].
- *  - Persistent lanes: a wave owns a contiguous range of candidates; a lane that finishes its
- *    candidate (after 64..~110 rounds) immediately takes the next one, so the wave never idles on its
- *    slowest lane until the range is exhausted.
- *  - The hash family is chosen per lane after the first ciphertext block; a wave runs the SHA-256 and
- *    SHA-512 paths predicated.
+ *  - AES T-tables: four rotated copies of Te0, 16 copies each, read by two lane groups from different tables so
+ *    every lookup is conflict-free and no rotates remain (aes128_encrypt_split); inner rounds as asm blocks.
+ *  - Slots and classes: a workgroup holds more candidates ("slots") than lanes, every slot's period and state in
+ *    LDS; a round runs for 64 queued slots of one hash class, so the SHA-256 / SHA-384 / SHA-512 choice and the
+ *    round's length never diverge inside a wave (the flow scheduler below, r6_claim).
+ *  - Persistent workgroups: a slot whose candidate finishes takes the next one from the launch's cursor.
  */
 #include "dev_crypto.h"
 #include "dprf_params.h"
@@ -30,45 +28,19 @@
 
 #include <mutex>
 
-/* T-tables in 256-byte rows, row x = entry x: R6_TABLES tables (table t = ror(Te0, 8t), or Te2 = ror16(Te0)
- * as the second of two), each replicated R6_TE_COPIES times; copy c of table t at byte 256*x +
- * 4*(c + t*copies), lane l reads copy l%copies.  The address of byte k of a state word is ONE v_perm: byte 1
- * <- byte k of the word, byte 0 <- 4*(lane%copies), bytes 2-3 <- 0 (+ the table's offset as an immediate).
- * Default: Te0 and Te2, 32 copies each, filling the rows: the 32 lanes of a ds_read_b32 half ({0-31},
- * {32-63}: MI355X_MICROARCH.md LDS table) meet 32 different banks, and a column needs one rotate instead of
- * three.  Measured (round 2, tools/ab_libs.sh pdf_r6): one table × 32 copies (conflict-free, slot periods in
- * the free row halves, 1,248 slots) 3.02 M cand/s; Te0 + Te2 × 16 copies in the row halves (2-way
- * conflicts, 1,248 slots) 3.18 M; Te0 + Te2 × 32 copies (no conflicts, 960 slots, all in the dynamic area)
- * 3.50 M; four tables × 16 copies (no rotates, 2-way conflicts, 960 slots) 3.06 M; four × 8 (4-way) 1.91 M.
- * Bank conflicts cost more than rotates or slots: they lengthen every round's dependent lookups.  With
- * R6_TE_USED <= 128 (fewer copies) bytes 128..255 of each row hold the periods of 32-slot groups
- * (slot_lds). */
+/* T-tables in 256-byte rows, row x = entry x: four tables T_t = ror(Te0, 8t), 16 copies each, copy c of T_t at byte
+ * 256 x + 4 (16 t + c); the address of a lookup is ONE v_perm (below).  Lane groups A (bit 4 of the lane clear) and B
+ * read different tables in every lookup, so the 32 lanes of a ds_read_b32 half ({0-31}, {32-63}: MI355X_MICROARCH.md
+ * LDS table) meet 32 different banks, and no rotates are left (aes128_encrypt_split).  Measured against the layouts of
+ * rounds 1-2 (one table x 32 copies 3.02 M cand/s, Te0 + Te2 x 32 copies 3.50 M, four tables x 8 copies 1.91 M: bank
+ * conflicts cost more than rotates; HISTORY.md) -- the split layout took R6 to 3.68 M in round 3. */
 #define R6_TE_ROW_BYTES 256
-/* R6_SPLIT (default, round 3): four tables x 16 copies, lane groups A (lanes with bit 4 clear) and B read different
- * tables in every lookup, so the 32 lanes of a ds_read_b32 half meet 32 banks, and no rotates are left (below,
- * aes128_encrypt_split). */
-#ifndef R6_SPLIT
-#define R6_SPLIT 1
-#endif
-#if R6_SPLIT
-#undef R6_TABLES
-#undef R6_TE_COPIES
 #define R6_TABLES 4
 #define R6_TE_COPIES 16
-#endif
-#ifndef R6_TABLES
-#define R6_TABLES 2
-#endif
-#ifndef R6_TE_COPIES
-#define R6_TE_COPIES (R6_TABLES == 4 ? 8 : 32)   /* 2 x 32: whole 256-byte rows, no bank conflicts */
-#endif
 #define R6_TE_BYTES (256 * R6_TE_ROW_BYTES)
-/* bytes of a row the tables take; the rest (when at least half a row) holds slot periods */
+/* bytes of a row the tables take (the whole row: no slot periods beside them, slot_lds te_slots = 0) */
 #define R6_TE_USED (4 * R6_TABLES * R6_TE_COPIES)
 static_assert(R6_TE_USED <= R6_TE_ROW_BYTES && (R6_TE_COPIES & (R6_TE_COPIES - 1)) == 0, "table rows");
-/* the table whose entry holds S[x] in bytes 3 and 0 (ror16 Te0): the key schedule and the last round
- * assemble S-box bytes from it and Te0 */
-#define R6_TE2 (R6_TABLES == 4 ? 2 : 1)
 
 DEVI uint32_t fastdiv6(uint32_t n, uint32_t m, uint32_t s) {
     uint32_t t = __umulhi(n, m);
@@ -98,104 +70,11 @@ struct r6_lds {
     uint32_t pat;              /* LDS byte address of the slot's group: rows of 256 bytes */
     uint32_t lanebase;         /* 4 * (slot % 64): the slot's column in the pattern area */
     uint32_t lanec;            /* 4 * (thread lane % R6_TE_COPIES): this thread's table copy */
-#if R6_SPLIT
     uint32_t base;             /* byte t: row offset of the copy of the table lookup t reads (A: T_t, B: T_t+1) */
-#endif
 };
 
-/* Te0[byte k of v] */
-template <int K>
-DEVI uint32_t teb(const r6_lds &S, uint32_t v) {
-    const uint32_t a = __builtin_amdgcn_perm(v, S.lanec, 0x0c0c0000u | ((4u + K) << 8));
-    return *(const uint32_t *)((const uint8_t *)r6_te + a);
-}
-/* table T (ror(Te0, 8T), or ror16 for T = 1 of two tables) [byte k of v]: its copies follow table T-1's */
-template <int T, int K>
-DEVI uint32_t tebt(const r6_lds &S, uint32_t v) {
-    const uint32_t a = __builtin_amdgcn_perm(v, S.lanec, 0x0c0c0000u | ((4u + K) << 8));
-    return *(const uint32_t *)((const uint8_t *)r6_te + 4 * R6_TE_COPIES * T + a);
-}
 DEVI uint32_t pat_addr(uint32_t pos, uint32_t lanebase) { return ((pos >> 2) << 8) | (pos & 3u) | lanebase; }
 
-DEVI void aes128_expand_te(const r6_lds &S, const uint32_t key[4], uint32_t rk[44]) {
-    const uint32_t rcon[10] = {0x01000000u, 0x02000000u, 0x04000000u, 0x08000000u, 0x10000000u,
-                               0x20000000u, 0x40000000u, 0x80000000u, 0x1b000000u, 0x36000000u};
-    rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-        const uint32_t t = rk[4 * i + 3];
-#if R6_TABLES >= 2
-        /* SubWord(RotWord(t)): S[x] in bytes 3, 0 of Te2[x] and 2, 1 of Te0[x] (see the last round) */
-        const uint32_t sw = perm(tebt<R6_TE2, 2>(S, t), teb<1>(S, t), 0x07020c0cu) | perm(teb<0>(S, t), tebt<R6_TE2, 3>(S, t), 0x0c0c0500u);
-#else
-        /* SubWord(RotWord(t)) with S[x] = byte 2 of Te0[x] */
-        const uint32_t sw = ((teb<2>(S, t) << 8) & 0xff000000u) | (teb<1>(S, t) & 0x00ff0000u) |
-                            ((teb<0>(S, t) >> 8) & 0x0000ff00u) | ((teb<3>(S, t) >> 16) & 0xffu);
-#endif
-        rk[4 * i + 4] = rk[4 * i] ^ sw ^ rcon[i];
-        rk[4 * i + 5] = rk[4 * i + 1] ^ rk[4 * i + 4];
-        rk[4 * i + 6] = rk[4 * i + 2] ^ rk[4 * i + 5];
-        rk[4 * i + 7] = rk[4 * i + 3] ^ rk[4 * i + 6];
-    }
-#if R6_TABLES == 2
-    /* the inner rounds add their key inside the ror8 of the two-table column: store it rotated back */
-#pragma unroll
-    for (int i = 4; i < 40; i++) rk[i] = ror32(rk[i], 24);
-#endif
-}
-
-DEVI void aes128_encrypt_te(const r6_lds &S, const uint32_t rk[44], uint32_t s0, uint32_t s1, uint32_t s2,
-                            uint32_t s3, uint32_t out[4]) {
-    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-#if R6_TABLES == 4
-        const uint32_t t0 = xor3(xor3(teb<3>(S, s0), tebt<1, 2>(S, s1), tebt<2, 1>(S, s2)), tebt<3, 0>(S, s3), rk[4 * r]);
-        const uint32_t t1 = xor3(xor3(teb<3>(S, s1), tebt<1, 2>(S, s2), tebt<2, 1>(S, s3)), tebt<3, 0>(S, s0), rk[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(teb<3>(S, s2), tebt<1, 2>(S, s3), tebt<2, 1>(S, s0)), tebt<3, 0>(S, s1), rk[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(teb<3>(S, s3), tebt<1, 2>(S, s0), tebt<2, 1>(S, s1)), tebt<3, 0>(S, s2), rk[4 * r + 3]);
-#elif R6_TABLES == 2
-        /* Te0[a] ^ ror8 Te0[b] ^ ror16 Te0[c] ^ ror24 Te0[d] ^ k = Te0[a] ^ Te2[c] ^ ror8(Te0[b] ^ Te2[d] ^ rol8 k) */
-        const uint32_t t0 = xor3(teb<3>(S, s0), tebt<1, 1>(S, s2), ror32(xor3(teb<2>(S, s1), tebt<1, 0>(S, s3), rk[4 * r]), 8));
-        const uint32_t t1 = xor3(teb<3>(S, s1), tebt<1, 1>(S, s3), ror32(xor3(teb<2>(S, s2), tebt<1, 0>(S, s0), rk[4 * r + 1]), 8));
-        const uint32_t t2 = xor3(teb<3>(S, s2), tebt<1, 1>(S, s0), ror32(xor3(teb<2>(S, s3), tebt<1, 0>(S, s1), rk[4 * r + 2]), 8));
-        const uint32_t t3 = xor3(teb<3>(S, s3), tebt<1, 1>(S, s1), ror32(xor3(teb<2>(S, s0), tebt<1, 0>(S, s2), rk[4 * r + 3]), 8));
-#else
-        const uint32_t t0 = xor3(xor3(teb<3>(S, s0), ror32(teb<2>(S, s1), 8), ror32(teb<1>(S, s2), 16)),
-                                 ror32(teb<0>(S, s3), 24), rk[4 * r]);
-        const uint32_t t1 = xor3(xor3(teb<3>(S, s1), ror32(teb<2>(S, s2), 8), ror32(teb<1>(S, s3), 16)),
-                                 ror32(teb<0>(S, s0), 24), rk[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(teb<3>(S, s2), ror32(teb<2>(S, s3), 8), ror32(teb<1>(S, s0), 16)),
-                                 ror32(teb<0>(S, s1), 24), rk[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(teb<3>(S, s3), ror32(teb<2>(S, s0), 8), ror32(teb<1>(S, s1), 16)),
-                                 ror32(teb<0>(S, s2), 24), rk[4 * r + 3]);
-#endif
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-#if R6_TABLES >= 2
-    /* last round: SubBytes + ShiftRows + AddRoundKey.  S[x] sits in bytes 2 and 1 of Te0[x] and in bytes 3
-     * and 0 of Te2[x], i.e. already where each output byte needs it: two v_perm and one or-xor per word */
-    {
-        const uint32_t HI = 0x07020c0cu, LO = 0x0c0c0500u;   /* src0.b3 src1.b2 0 0 | 0 0 src0.b1 src1.b0 */
-        out[0] = (perm(tebt<R6_TE2, 3>(S, s0), teb<2>(S, s1), HI) | perm(teb<1>(S, s2), tebt<R6_TE2, 0>(S, s3), LO)) ^ rk[40];
-        out[1] = (perm(tebt<R6_TE2, 3>(S, s1), teb<2>(S, s2), HI) | perm(teb<1>(S, s3), tebt<R6_TE2, 0>(S, s0), LO)) ^ rk[41];
-        out[2] = (perm(tebt<R6_TE2, 3>(S, s2), teb<2>(S, s3), HI) | perm(teb<1>(S, s0), tebt<R6_TE2, 0>(S, s1), LO)) ^ rk[42];
-        out[3] = (perm(tebt<R6_TE2, 3>(S, s3), teb<2>(S, s0), HI) | perm(teb<1>(S, s1), tebt<R6_TE2, 0>(S, s2), LO)) ^ rk[43];
-        return;
-    }
-#endif
-    /* last round: SubBytes + ShiftRows + AddRoundKey, S[x] = byte 2 of Te0[x] */
-    out[0] = (((teb<3>(S, s0) << 8) & 0xff000000u) | (teb<2>(S, s1) & 0x00ff0000u) |
-              ((teb<1>(S, s2) >> 8) & 0x0000ff00u) | ((teb<0>(S, s3) >> 16) & 0xffu)) ^ rk[40];
-    out[1] = (((teb<3>(S, s1) << 8) & 0xff000000u) | (teb<2>(S, s2) & 0x00ff0000u) |
-              ((teb<1>(S, s3) >> 8) & 0x0000ff00u) | ((teb<0>(S, s0) >> 16) & 0xffu)) ^ rk[41];
-    out[2] = (((teb<3>(S, s2) << 8) & 0xff000000u) | (teb<2>(S, s3) & 0x00ff0000u) |
-              ((teb<1>(S, s0) >> 8) & 0x0000ff00u) | ((teb<0>(S, s1) >> 16) & 0xffu)) ^ rk[42];
-    out[3] = (((teb<3>(S, s3) << 8) & 0xff000000u) | (teb<2>(S, s0) & 0x00ff0000u) |
-              ((teb<1>(S, s1) >> 8) & 0x0000ff00u) | ((teb<0>(S, s2) >> 16) & 0xffu)) ^ rk[43];
-}
-
-#if R6_SPLIT
 /* Lane-group split AES (round 3).  Four tables T_t = ror(Te0, 8t), 16 copies each: copy c of T_t is dword 16t + c
  * of every 256-byte row, so it sits in bank (16t + c) mod 32 of a ds_read_b32 (MI355X_MICROARCH.md LDS table).
  * Lanes l (c = l % 16) form group A (bit 4 of l clear) and group B (set): in every lookup A reads T_t and B T_t+1,
@@ -251,33 +130,21 @@ DEVI void aes128_expand_split(const r6_lds &S, const uint32_t key[4], uint32_t r
  * three-way XORs (v_bitop3 0x96) behind the wait that covers its four reads.  LLVM's schedule of the same dataflow keeps 1-2 reads in flight
  * per wait (the kernel sits at its VGPR limit) and exposes the LDS latency several times per round.  The block
  * ends with every read consumed, so no LDS operation of it is in flight for the compiler's own waits. */
-#ifndef R6_ASM_ROUND
-#define R6_ASM_ROUND 1
-#endif
 #define R6_SEL(t) (0x0c0c0000u | ((4u + 3u - (t)) << 8) | (t))
-/* R6_B1_BITOP3 (round 4, default): the four lookups per round that take byte 1 of a state word (term t = 2) form their
+/* The four lookups per round that take byte 1 of a state word (term t = 2) form their
  * address as (s & 0xff00) | (base >> 16 without its byte 1) -- ONE v_bitop3 (truth table 0xe2, full rate on gfx950
  * with two VGPR sources) instead of a v_perm (half rate); base >> 16 is formed once per round inside the block (a
  * long-lived register for it made the kernel spill 12 B/lane).  Measured: 3.743 -> 3.753 M cand/s (three alternating
  * runs, profiles/ab_r6_b1_bitop3_r04t.txt).  The other three terms need a shift first (v_lshrrev + v_bitop3 for bytes
  * 2 and 3, a half-rate v_lshlrev for byte 0): no fewer cycles than the v_perm. */
-#ifndef R6_B1_BITOP3
-#define R6_B1_BITOP3 1
-#endif
 DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
                        uint32_t k1, uint32_t k2, uint32_t k3) {
     uint32_t t[16];
 #define R6L(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
-#if R6_B1_BITOP3
     /* base >> 16 in t[15]'s register: its own lookup (the last of the 16) comes after the four that read it */
 #define R6_B2PRE "v_lshrrev_b32 %19, 16, %20\n\t"
 #define R6L2(d, s) "v_bitop3_b32 %" #d ", %" #s ", %29, %19 bitop3:0xe2\n\tds_read_b32 %" #d ", %" #d "\n\t"
 #define R6_B2IN , "s"(0xff00u)
-#else
-#define R6_B2PRE
-#define R6L2(d, s) R6L(d, s, 27)
-#define R6_B2IN
-#endif
     asm volatile(
         /* column 0: s0 t0, s1 t1, s2 t2, s3 t3;  column 1: s1, s2, s3, s0;  column 2: s2, s3, s0, s1;  column 3 */
         R6_B2PRE
@@ -309,78 +176,21 @@ DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, u
 #undef R6L
 }
 
-/* The last round the same way: 16 lookups, then per column the two v_perm that place its four S-box bytes and one
- * v_bitop3 (a | b) ^ k (truth table 0x56).  Lookup byte p of s_(j+3-p) through base byte 1-p; LO = 0x0c0c0500 is
- * also the selector of the p = 1 lookup. */
-#ifndef R6_ASM_LAST
-#define R6_ASM_LAST 0               /* measured round 3: 3.666 vs 3.678 M cand/s with the compiler's last round */
-#endif
-#define R6_SELL(p) (0x0c0c0000u | ((4u + (p)) << 8) | ((1u - (p)) & 3u))
-DEVI void r6_last_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t base, uint32_t k0,
-                      uint32_t k1, uint32_t k2, uint32_t k3) {
-    uint32_t t[16];
-#define R6L(d, s, sel) "v_perm_b32 %" #d ", %" #s ", %20, %" #sel "\n\tds_read_b32 %" #d ", %" #d "\n\t"
-#define R6C(a, b, c, d, o, k)                                                                                      \
-    "v_perm_b32 %" #a ", %" #a ", %" #b ", %29\n\t"                                                              \
-    "v_perm_b32 %" #c ", %" #c ", %" #d ", %27\n\t"                                                              \
-    "v_bitop3_b32 %" #o ", %" #a ", %" #c ", %" #k " bitop3:0x56\n\t"
-    asm volatile(
-        /* column j: byte 3 from s_j, byte 2 from s_j+1, byte 1 from s_j+2, byte 0 from s_j+3; selectors %25..%28 are
-         * bytes p = 3, 2, 1, 0 */
-        R6L(4, 0, 25) R6L(5, 1, 26) R6L(6, 2, 27) R6L(7, 3, 28)
-        R6L(8, 1, 25) R6L(9, 2, 26) R6L(10, 3, 27) R6L(11, 0, 28)
-        R6L(12, 2, 25) R6L(13, 3, 26) R6L(14, 0, 27) R6L(15, 1, 28)
-        R6L(16, 3, 25) R6L(17, 0, 26) R6L(18, 1, 27) R6L(19, 2, 28)
-        "s_waitcnt lgkmcnt(12)\n\t"
-        R6C(4, 5, 6, 7, 0, 21)
-        "s_waitcnt lgkmcnt(8)\n\t"
-        R6C(8, 9, 10, 11, 1, 22)
-        "s_waitcnt lgkmcnt(4)\n\t"
-        R6C(12, 13, 14, 15, 2, 23)
-        "s_waitcnt lgkmcnt(0)\n\t"
-        R6C(16, 17, 18, 19, 3, 24)
-        : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]),
-          "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]),
-          "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
-        : "v"(base), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(R6_SELL(3)), "s"(R6_SELL(2)), "s"(R6_SELL(1)),
-          "s"(R6_SELL(0)), "s"(0x07020c0cu)
-        : "memory");
-#undef R6C
-#undef R6L
-}
-
 DEVI void aes128_encrypt_split(const r6_lds &S, const uint32_t rk[44], uint32_t s0, uint32_t s1, uint32_t s2,
                                uint32_t s3, uint32_t out[4]) {
     uint32_t s[4] = {s0 ^ rk[0], s1 ^ rk[1], s2 ^ rk[2], s3 ^ rk[3]};
 #pragma unroll
-    for (int r = 1; r < 10; r++) {
-        if (R6_ASM_ROUND) {
-            r6_round_asm(s[0], s[1], s[2], s[3], S.base, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3]);
-            continue;
-        }
-        uint32_t n[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            n[j] = xor3(xor3(r6_ld<3, 0>(s[j], S.base), r6_ld<2, 1>(s[(j + 1) & 3], S.base),
-                             r6_ld<1, 2>(s[(j + 2) & 3], S.base)),
-                        r6_ld<0, 3>(s[(j + 3) & 3], S.base), rk[4 * r + j]);
-#pragma unroll
-        for (int j = 0; j < 4; j++) s[j] = n[j];
-    }
+    for (int r = 1; r < 10; r++)
+        r6_round_asm(s[0], s[1], s[2], s[3], S.base, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3]);
     /* last round: byte p of word j <- S[byte p of s_(j+3-p)] (B: of its rotated registers) through base byte 1-p
-     * (A: T_1-p, B: T_2-p, both with S at byte p), combined as before */
+     * (A: T_1-p, B: T_2-p, both with S at byte p), combined as before (the compiler's schedule: an asm block like the
+     * inner rounds' measured 3.666 vs 3.678 M cand/s, round 3) */
     uint32_t acc[4];
-    if (R6_ASM_LAST) {
-        r6_last_asm(s[0], s[1], s[2], s[3], S.base, rk[40], rk[41], rk[42], rk[43]);
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[j] = s[j];
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            acc[j] = (perm(r6_ld<3, 2>(s[j], S.base), r6_ld<2, 3>(s[(j + 1) & 3], S.base), 0x07020c0cu) |
-                      perm(r6_ld<1, 0>(s[(j + 2) & 3], S.base), r6_ld<0, 1>(s[(j + 3) & 3], S.base), 0x0c0c0500u)) ^
-                     rk[40 + j];
-    }
+    for (int j = 0; j < 4; j++)
+        acc[j] = (perm(r6_ld<3, 2>(s[j], S.base), r6_ld<2, 3>(s[(j + 1) & 3], S.base), 0x07020c0cu) |
+                  perm(r6_ld<1, 0>(s[(j + 2) & 3], S.base), r6_ld<0, 1>(s[(j + 3) & 3], S.base), 0x0c0c0500u)) ^
+                 rk[40 + j];
     /* B's word j holds ror(out[j + 1], 8): out[j] = rol(acc[j - 1], 8).  The selector is derived from base here
      * rather than kept in a register across the round (the kernel sits at its 168-VGPR limit) */
     const uint32_t selr = (S.base & 0x40u) ? 0x02010003u : 0x07060504u;
@@ -389,10 +199,6 @@ DEVI void aes128_encrypt_split(const r6_lds &S, const uint32_t rk[44], uint32_t 
 }
 #define R6_EXPAND aes128_expand_split
 #define R6_ENCRYPT aes128_encrypt_split
-#else
-#define R6_EXPAND aes128_expand_te
-#define R6_ENCRYPT aes128_encrypt_te
-#endif
 
 /* SHA-512 over 32 BE words held as two 16-word halves; state as 16 BE words (hi, lo pairs) */
 DEVI void sha512_compress_pairs(uint32_t hs[16], const uint32_t lo[16], const uint32_t hi[16]) {
@@ -713,12 +519,10 @@ DEVI r6_lds slot_lds(uint32_t patbase, uint32_t pat_words, uint32_t te_slots, ui
         S.lanebase = (t & 63u) << 2;
     }
     S.lanec = (lane & (R6_TE_COPIES - 1u)) << 2;
-#if R6_SPLIT
     /* copy c = lane % 16 in every byte; table offsets 64 t: A (lane bit 4 clear) T_t / B T_t+1 for lookup t */
     const uint32_t c4 = S.lanec * 0x01010101u;
     const bool gb = (lane & 16u) != 0u;
     S.base = c4 + (gb ? 0x00c08040u : 0xc0804000u);
-#endif
     return S;
 }
 
@@ -845,12 +649,11 @@ k_pdf_r6(dprf_enum e, dprf_pdf_params p, const dprf_aes_tables *T, dprf_results 
         if (tid == 0) atomicOr(&R->pad_, 8u);
         return;
     }
-    /* the tables' copies fill the first R6_TE_USED bytes of each row: table t = ror(Te0, 8t) (16t with two
-     * tables); the rest of a row, if any, holds slot periods */
+    /* the tables' copies fill each row: table t = ror(Te0, 8t) */
     constexpr uint32_t TW = R6_TE_USED / 4;                                     /* table words per row */
     for (uint32_t k = tid; k < 256u * TW; k += nthr) {
         const uint32_t x = k / TW, c = k % TW, t = c / R6_TE_COPIES;
-        r6_te[x * (R6_TE_ROW_BYTES / 4) + c] = ror32(T->te0[x], (R6_TABLES == 2 ? 16 : 8) * t);
+        r6_te[x * (R6_TE_ROW_BYTES / 4) + c] = ror32(T->te0[x], 8 * t);
     }
     for (uint32_t k = tid; k < 64; k += nthr) ((uint32_t *)cs)[k] = ((const uint32_t *)e.charset)[k];
     for (uint32_t k = tid; k < R6_QUEUES * R6_MAP_WORDS; k += nthr) (&sh->map[0][0])[k] = 0u;
