@@ -184,3 +184,21 @@ def test_issue_line_from_a_profile():
     assert i["instr_floor"] == work.per_candidate("odt", "instr", "main")
     assert abs(i["instr_frac"] - i["instr_floor"] / 2370181.0) < 1e-12 and i["cycles_per_instr"] == 3.936
     assert bench.issue_line(None, "pdf_r6", 6) == {"instr_floor": work.per_candidate("pdf_r6", "instr", "main")}
+
+
+def test_r6_instruction_breakdown_record():
+    """profiles/r6_instr_breakdown_r06.json (tools/r6_instr_breakdown.py): the R6 kernel's measured VALU instructions
+    per candidate attributed by primitive from probe kernels of its own device code -- the record is consistent with
+    work.COUNTS / work.INSTR and leaves under 2 % of the measured count to the slot scheduler."""
+    import json
+    import os
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "..", "profiles", "r6_instr_breakdown_r06.json")))
+    rows = d["rows"]
+    assert rows["sha256c"]["units"] == work.COUNTS["pdf_r6"]["sha256c"]
+    assert rows["aes_block"]["floor_per_unit"] == work.INSTR["aes128_enc_block"]
+    assert abs(sum(r["per_candidate"] for r in rows.values()) - d["attributed_per_candidate"]) < 1e-3
+    assert 0 <= d["unattributed_frac"] < 0.02
+    # the primitives run at their instruction floors but AES (a few percent above)
+    assert abs(rows["sha256c"]["per_unit"] / work.INSTR["sha256c"] - 1) < 0.01
+    assert abs(rows["sha512c"]["per_unit"] / work.INSTR["sha512c"] - 1) < 0.01
+    assert 1.0 <= rows["aes_block"]["per_unit"] / work.INSTR["aes128_enc_block"] < 1.15
