@@ -33,6 +33,10 @@ CASES = [
     ("0123456789abcdef", "c0ffee5"),  # cslen 16: runs of 16 through the wrap
     ("0123456789", "20241231"),     # digits: runs of 8
     ("ab", "abbabaabbabaabbabab"),  # 19 chars: the generic instantiation; cslen < 8: per-candidate path
+    # 17-32 characters on the RUN path (the 8-word instantiation with runs had no case)
+    ("0123456789", "31415926535897932"),              # 17 chars, runs of 8, byte 0 of word 4
+    ("0123456789abcdef", "0" * 20 + "deadbeefca1"),   # 31 chars, runs of 16, byte 2 of word 7
+    ("abcdefgh", "a" * 28 + "hgcb"),                  # 32 chars: the last slot byte, runs of 8
     ("0123456", "6543210"),         # cslen 7: per-candidate path
 ]
 
@@ -93,6 +97,7 @@ def test_cases_cover_the_run_shapes():
     assert nw == {1, 2, 3, 4, 8}
     assert {(len(pw) - 1) % 4 for _, pw in CASES} == {0, 1, 2, 3}
     assert {len(cs) for cs, _ in CASES} >= {7, 8, 10, 16, 26, 62}
+    assert {len(pw) for cs, pw in CASES if len(cs) >= 8 and len(pw) > 16} == {17, 31, 32}
 
 
 @pytest.mark.parametrize("cs,pw", CASES, ids=[pw for _, pw in CASES])
