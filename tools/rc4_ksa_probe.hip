@@ -107,6 +107,79 @@ __global__ void __launch_bounds__(128) k_time2(const uint32_t *keys, uint32_t *s
     __syncthreads();
 }
 
+/* Mode "tenth" (round 6, VERDICT r5 Next #6): would a 10th, quarter-width RC4 chain per CU add throughput?  Nine
+ * product-shape workgroups (k_time2, 16 KiB of S-boxes each) leave ~6 KiB of a CU's ~152 KiB allocatable LDS; a wave
+ * whose 16 active lanes own 256-byte S-boxes in 64-byte rows (4 KiB) fits there.  k_quarter is that wave: one 64-thread
+ * workgroup per CU, lanes 16-63 retire at once (an idle lane is not skipped at issue, so the wave costs a full wave's
+ * issue time per instruction), the KSA as a plain per-step loop on the 64-byte rows (the asm block assumes 256-byte
+ * rows: its S[j] address is a byte insert).  Launched beside the nine on a second stream, it measures how much the
+ * nine chains slow down with a tenth wave resident -- the cost side of the trade -- and what the quarter chain adds. */
+template <int NK>
+__global__ void __launch_bounds__(64) k_quarter(const uint32_t *keys, uint32_t *sink, int passes) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[16 * 256];
+    const uint32_t lane = threadIdx.x;
+    if (lane >= 16u) return;
+    const size_t g = (size_t)blockIdx.x * 16u + lane;
+    uint8_t *box = S + 4u * lane;                                     /* byte i at row i/4 (64 B), column 4 lane + i%4 */
+    auto at = [&](uint32_t i) -> uint8_t & { return box[((i >> 2) << 6) + (i & 3u)]; };
+    uint32_t k[4] = {keys[4 * (g & 4095)], keys[4 * (g & 4095) + 1], keys[4 * (g & 4095) + 2], keys[4 * (g & 4095) + 3]};
+    uint32_t acc = 0;
+    for (int x = 0; x < passes; x++) {
+        for (uint32_t i = 0; i < 256u; i++) at(i) = (uint8_t)i;
+        uint32_t j = 0;
+#pragma unroll 8
+        for (uint32_t i = 0; i < 256u; i++) {
+            const uint32_t si = at(i);
+            j = (j + si + (((k[(i % NK) >> 2] >> (8 * ((i % NK) & 3u))) ^ (uint32_t)x) & 0xffu)) & 0xffu;
+            const uint32_t sj = at(j);
+            at(i) = (uint8_t)sj;
+            at(j) = (uint8_t)si;
+        }
+        acc += at(1) + at(2);                                         /* the PRGA-2 reads, roughly */
+    }
+    sink[g] = acc;
+}
+
+static void time_tenth(int passes, int qpasses) {
+    int ncu = 0;
+    CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    std::vector<uint32_t> keys(4096 * 4);
+    uint64_t st = 0x243F6A8885A308D3ull;
+    for (auto &w : keys) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; w = (uint32_t)st; }
+    uint32_t *dk, *ds, *dq;
+    CHECK(hipMalloc(&dk, keys.size() * 4));
+    CHECK(hipMalloc(&ds, (size_t)ncu * 9 * 64 * 4));
+    CHECK(hipMalloc(&dq, (size_t)ncu * 16 * 4));
+    CHECK(hipMemcpy(dk, keys.data(), keys.size() * 4, hipMemcpyHostToDevice));
+    hipStream_t s1, s2;
+    CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t a1, b1, a2, b2;
+    CHECK(hipEventCreate(&a1)); CHECK(hipEventCreate(&b1)); CHECK(hipEventCreate(&a2)); CHECK(hipEventCreate(&b2));
+    for (int r = 0; r < 8; r++) hipLaunchKernelGGL((k_time2<16, 3>), dim3(ncu * 9), dim3(128), 0, s1, dk, ds, passes);
+    CHECK(hipDeviceSynchronize());
+    for (int rep = 0; rep < 3; rep++) {
+        for (int mode = 0; mode < 3; mode++) {                        /* 0: nine alone, 1: quarter alone, 2: both */
+            float m1 = 0, m2 = 0;
+            if (mode != 1) CHECK(hipEventRecord(a1, s1));
+            if (mode != 0) CHECK(hipEventRecord(a2, s2));
+            if (mode != 1) hipLaunchKernelGGL((k_time2<16, 3>), dim3(ncu * 9), dim3(128), 0, s1, dk, ds, passes);
+            if (mode != 0) hipLaunchKernelGGL((k_quarter<16>), dim3(ncu), dim3(64), 0, s2, dk, dq, qpasses);
+            if (mode != 1) CHECK(hipEventRecord(b1, s1));
+            if (mode != 0) CHECK(hipEventRecord(b2, s2));
+            CHECK(hipDeviceSynchronize());
+            if (mode != 1) CHECK(hipEventElapsedTime(&m1, a1, b1));
+            if (mode != 0) CHECK(hipEventElapsedTime(&m2, a2, b2));
+            const double nine = mode != 1 ? (double)ncu * 9 * 64 * passes / 20.0 / (m1 * 1e-3) : 0;
+            const double quarter = mode != 0 ? (double)ncu * 16 * qpasses / 20.0 / (m2 * 1e-3) : 0;
+            printf("{\"mode\": \"%s\", \"rep\": %d, \"nine_ms\": %.3f, \"quarter_ms\": %.3f, "
+                   "\"nine_cand_per_s\": %.4g, \"quarter_cand_per_s\": %.4g}\n",
+                   mode == 0 ? "nine alone" : mode == 1 ? "quarter alone" : "nine + quarter", rep, m1, m2, nine, quarter);
+        }
+    }
+    CHECK(hipFree(dk)); CHECK(hipFree(ds)); CHECK(hipFree(dq));
+}
+
 template <int NK, int R>
 static void time_passes2(int passes) {
     int ncu = 0;
@@ -275,6 +348,13 @@ static int run(int blocks, int passes) {
 }
 
 int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "tenth")) {         /* rc4_ksa_probe tenth [passes] [quarter passes] */
+        const int passes = argc > 2 ? atoi(argv[2]) : 2000;
+        const int qpasses = argc > 3 ? atoi(argv[3]) : 600;
+        if (passes < 1 || passes > 100000 || qpasses < 1 || qpasses > 100000) { printf("bad args\n"); return 2; }
+        time_tenth(passes, qpasses);
+        return 0;
+    }
     if (argc > 1 && !strcmp(argv[1], "time2")) {         /* rc4_ksa_probe time2 [passes] */
         const int passes = argc > 2 ? atoi(argv[2]) : 4000;
         if (passes < 1 || passes > 100000) { printf("bad args\n"); return 2; }
