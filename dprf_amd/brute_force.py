@@ -198,12 +198,14 @@ def search_round(ctx, charset, pwlen, start, count, stop_on_first=True):
     if check_charset(charset):
         hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
         return (hits[0] if hits else None), st
-    from .payload import spell_utf8
+    import os
+    from .payload import spell_utf8_parallel
     total = {"candidates": 0, "wall_ms": 0.0}
     found = None
+    workers = min(16, os.cpu_count() or 1)
     for s in range(start, start + count, WIDE_ROUND):
         n = min(WIDE_ROUND, start + count - s)
-        blob, offs = spell_utf8(charset, pwlen, s, n)
+        blob, offs = spell_utf8_parallel(charset, pwlen, s, n, workers)
         hits, _, st = ctx.verify_blob(blob, offs, stop_on_first=stop_on_first, cap=1)
         total["candidates"] += st["candidates"]
         total["wall_ms"] += st["wall_ms"]

@@ -175,6 +175,15 @@ def test_check_charset_rules():
         assert ei.value.code == _lib.E_CHARSET, bad
 
 
+def test_spell_utf8_parallel_equals_one_thread():
+    from dprf_amd.payload import spell_utf8, spell_utf8_parallel
+    cs = "abcäöü€\U0001F600"
+    for start, count in ((0, 5000), (123457, 40001), (8 ** 5 - 10, 10)):
+        b1, o1 = spell_utf8(cs, 6, start, count)
+        b2, o2 = spell_utf8_parallel(cs, 6, start, count, workers=4, part=4096)
+        assert b1 == b2 and (o1 == o2).all(), (start, count)
+
+
 @pytest.mark.parametrize("cs,n", [("aé", 3), ("x€y\U0001F600", 2), ("ab", 4), ("é", 2)])
 def test_spell_utf8_is_itertools_product(cs, n):
     from dprf_amd.payload import spell_utf8
