@@ -176,9 +176,11 @@ DEVI void r6_round_asm(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, u
 #undef R6L
 }
 
-DEVI void aes128_encrypt_split(const r6_lds &S, const uint32_t rk[44], uint32_t s0, uint32_t s1, uint32_t s2,
-                               uint32_t s3, uint32_t out[4]) {
-    uint32_t s[4] = {s0 ^ rk[0], s1 ^ rk[1], s2 ^ rk[2], s3 ^ rk[3]};
+/* E(v ^ iv): the CBC xor and the first AddRoundKey as one v_bitop3 per word (LLVM emits two v_xor) */
+DEVI void aes128_encrypt_split(const r6_lds &S, const uint32_t rk[44], const uint32_t v[4], const uint32_t iv[4],
+                               uint32_t out[4]) {
+    uint32_t s[4] = {xor3(v[0], iv[0], rk[0]), xor3(v[1], iv[1], rk[1]), xor3(v[2], iv[2], rk[2]),
+                     xor3(v[3], iv[3], rk[3])};
 #pragma unroll
     for (int r = 1; r < 10; r++)
         r6_round_asm(s[0], s[1], s[2], s[3], S.base, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3]);
@@ -347,7 +349,7 @@ DEVI uint32_t r6_family(const r6_lds &S, uint32_t len) {
     r6_load_k(S, len, K);
     R6_EXPAND(S, K, rk);
     r6_read16(S, 0u, v);
-    R6_ENCRYPT(S, rk, v[0] ^ K[4], v[1] ^ K[5], v[2] ^ K[6], v[3] ^ K[7], y);
+    R6_ENCRYPT(S, rk, v, K + 4, y);
     uint32_t sum = __builtin_amdgcn_sad_u8(y[0], 0u, 0u);
     sum = __builtin_amdgcn_sad_u8(y[1], 0u, sum);
     sum = __builtin_amdgcn_sad_u8(y[2], 0u, sum);
@@ -399,7 +401,7 @@ DEVI uint32_t r6_round(const r6_lds &S, uint32_t len, uint32_t &bs, uint32_t hse
             } else {
                 r6_read16(S, o, v);
             }
-            R6_ENCRYPT(S, rk, v[0] ^ prev[0], v[1] ^ prev[1], v[2] ^ prev[2], v[3] ^ prev[3], y);
+            R6_ENCRYPT(S, rk, v, prev, y);
 #pragma unroll
             for (int k = 0; k < 4; k++) { prev[k] = y[k]; w[4 * q + k] = y[k]; }
             o += 16u;

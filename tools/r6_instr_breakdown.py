@@ -39,9 +39,10 @@ extern "C" __global__ void __launch_bounds__(768, 1) probe_empty(uint32_t *io) {
 /* one AES-128 block of a round: CBC xor + the split-table cipher (R6_ENCRYPT), output to the SHA message */
 extern "C" __global__ void __launch_bounds__(768, 1) probe_aes_block(uint32_t *io) {
     const r6_lds S = probe_lds(io);
-    uint32_t rk[44], y[4];
+    uint32_t rk[44], v[4], iv[4], y[4];
     for (int k = 0; k < 44; k++) rk[k] = IN(8 + k);
-    R6_ENCRYPT(S, rk, IN(60) ^ IN(64), IN(61) ^ IN(65), IN(62) ^ IN(66), IN(63) ^ IN(67), y);
+    for (int k = 0; k < 4; k++) { v[k] = IN(60 + k); iv[k] = IN(64 + k); }
+    R6_ENCRYPT(S, rk, v, iv, y);
     for (int k = 0; k < 4; k++) OUT(k, y[k]);
 }
 /* one 16-byte block read from the slot's period column, range mode (r6_round UNI: 4 or 5 LDS words + 4 v_perm) */

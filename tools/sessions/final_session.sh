@@ -2,7 +2,7 @@
 # The end-of-round GPU session (gpurun): GPU tests, smoke, rocprof of every workload on THIS build, the profiles
 # installed into profiles/ (box-local) so that the bench line that follows reads counters of the same build
 # ("stale": false), then the bench line.  Everything to keep is copied under gpurun_out/.
-# Usage (on the box, from the repo root): tools/final_session.sh <tag>
+# Usage (on the box, from the repo root): tools/sessions/final_session.sh <tag>
 set -e
 TAG=${1:?tag}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
