@@ -10,7 +10,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPRF_LIB") or os.path.join(HERE, "libdprf.so")   # DPRF_LIB: A/B builds only
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 ALL_DEVICES = -1
 FMT_OFFICE, FMT_ODT, FMT_PDF = 1, 2, 3
 E_INVALID, E_DOMAIN, E_HIP, E_NODEVICE, E_PWLEN, E_CHARSET = -1, -2, -3, -4, -5, -6
@@ -20,7 +20,7 @@ MAX_PW, MAX_PW_RANGE, MAX_PW_R6 = 131071, 32, 176
 EXPORTS = ["dprf_abi_version", "dprf_last_error", "dprf_device_count", "dprf_device_list", "dprf_ctx_create",
            "dprf_ctx_create_devices", "dprf_ctx_destroy", "dprf_ctx_format", "dprf_ctx_flags", "dprf_ctx_kernel",
            "dprf_ctx_devices", "dprf_search_range", "dprf_verify_list", "dprf_list_status", "dprf_build_id",
-           "dprf_plan_chunk", "dprf_ctx_last_call_devices"]
+           "dprf_plan_chunk", "dprf_ctx_last_call_devices", "dprf_search_symbols"]
 
 
 class DprfError(RuntimeError):
@@ -86,6 +86,11 @@ def lib():
                                             ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
             L.dprf_search_range.restype = ctypes.c_int
+            L.dprf_search_symbols.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32),
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64,
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
+            L.dprf_search_symbols.restype = ctypes.c_int
             L.dprf_verify_list.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(Stats)]
@@ -203,7 +208,7 @@ class Context:
         byte symbols (include/dprf.h dprf_search_range)."""
         if isinstance(charset, str) and any(ord(ch) >= 0x80 for ch in charset):
             raise DprfError(E_CHARSET, "search_range enumerates byte symbols: charset %r has multi-byte characters "
-                                       "(brute_force.search_round verifies such windows in list mode)" % charset)
+                                       "(search_symbols enumerates characters)" % charset)
         cs = _to_bytes(charset)
         hits = (ctypes.c_uint64 * max(1, cap))()
         nh = ctypes.c_int64()
@@ -211,6 +216,23 @@ class Context:
         _check(lib().dprf_search_range(self._h, cs, len(cs), int(pwlen), int(start), int(count),
                                        1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
         return list(hits[:min(nh.value, cap)]), nh.value, st.as_dict()
+
+    def search_symbols(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
+        """Verify keyspace indices [start, start+count) of charset^pwlen over the CHARACTERS of a str charset (each
+        symbol its UTF-8 bytes; for Office the library converts each to UTF-16LE), spelled on the device (ABI 7,
+        include/dprf.h dprf_search_symbols).  Returns (sorted hit indices -- keyspace indices, like search_range's --,
+        total hits, stats dict).  DprfError(E_PWLEN) when a candidate could exceed a 64-byte list slot."""
+        syms = [ch.encode("utf-8") for ch in charset] if isinstance(charset, str) else [bytes([b]) for b in charset]
+        offs = [0]
+        for b in syms:
+            offs.append(offs[-1] + len(b))
+        so = (ctypes.c_uint32 * len(offs))(*offs)
+        hits = (ctypes.c_uint64 * max(1, cap))()
+        nh = ctypes.c_int64()
+        st = Stats()
+        _check(lib().dprf_search_symbols(self._h, b"".join(syms), so, len(syms), int(pwlen), int(start), int(count),
+                                         1 if stop_on_first else 0, hits, cap, ctypes.byref(nh), ctypes.byref(st)))
+        return [int(start) + h for h in hits[:min(nh.value, cap)]], nh.value, st.as_dict()
 
     def verify_blob(self, blob, offsets, stop_on_first=False, cap=1 << 16):
         """verify_list without per-candidate Python work: candidate k is blob[offsets[k]:offsets[k+1]]

@@ -194,10 +194,19 @@ def search_round(ctx, charset, pwlen, start, count, stop_on_first=True):
     """One round of range mode on every device of ctx: (lowest hit index or None, stats).  The same call
     bench.py times per rank (there with stop_on_first=False: a throughput step verifies its whole batch
     even when a false positive of ODF -e's 2-byte check turns up in it).  A charset with multi-byte characters
-    (check_charset False) is spelled on the host and verified as a list, in calls of WIDE_ROUND candidates."""
+    (check_charset False) is enumerated by character: spelled on the device (ctx.search_symbols, ABI 7) when every
+    candidate fits a 64-byte list slot, else spelled on the host and verified as a list, in calls of WIDE_ROUND
+    candidates."""
     if check_charset(charset):
         hits, _, st = ctx.search_range(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
         return (hits[0] if hits else None), st
+    if hasattr(ctx, "search_symbols"):
+        try:
+            hits, _, st = ctx.search_symbols(charset, pwlen, start, count, stop_on_first=stop_on_first, cap=1)
+            return (hits[0] if hits else None), st
+        except _lib.DprfError as ex:
+            if ex.code != _lib.E_PWLEN:
+                raise
     import os
     from .payload import spell_utf8_parallel
     total = {"candidates": 0, "wall_ms": 0.0}

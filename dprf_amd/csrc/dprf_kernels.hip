@@ -219,6 +219,54 @@ k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, 
     for (int k = 0; k < 8; k++)
         if (k < 5 || !sha1) e.keys[(size_t)k * e.count + g] = h[k];
 }
+
+/* ================================================================== symbol windows (round 6) */
+/* Range mode over a charset whose symbols take several bytes (a --charset with non-ASCII characters: one symbol per
+ * character, its UTF-8 -- for Office its UTF-16LE -- bytes): index g of the chunk -> the candidate's bytes in a list
+ * slot, in itertools.product order over the symbols (brute_force.py:205), for the list-mode kernels to verify.  The
+ * digits come as in range_candidate (the chunk start's digits from the host, g added with carries); the bytes are
+ * assembled in the thread's column of an LDS tile ([word][thread]: conflict-free) and stored as four 16-byte words.
+ * Bytes at or past `trunc` (PDF R2-R4 hash 32, pdf...c:137) and past the slot are never written: the slot stays zero
+ * there, as dprf_verify_list packs a truncated candidate. */
+__global__ void __launch_bounds__(256)
+k_spell_symbols(dprf_enum e, const uint32_t *symtab, uint32_t trunc, uint32_t *slots, uint8_t *lens) {
+    __shared__ uint32_t sym[256], syl[256];
+    __shared__ uint32_t tile[DPRF_SLOT_WORDS * 256];
+    __shared__ uint8_t dig[DPRF_MAX_RANGE_LEN * 256];
+    const uint32_t tid = threadIdx.x;
+    sym[tid] = symtab[tid];
+    syl[tid] = symtab[256 + tid];
+#pragma unroll
+    for (int j = 0; j < DPRF_SLOT_WORDS; j++) tile[j * 256 + tid] = 0u;
+    __syncthreads();
+    const uint32_t g = blockIdx.x * 256u + tid;
+    if (g >= e.count) return;
+    const uint32_t n = e.pwlen < DPRF_MAX_RANGE_LEN ? e.pwlen : DPRF_MAX_RANGE_LEN;
+    uint32_t rem = g, carry = 0;
+    for (int p = (int)n - 1; p >= 0; --p) {
+        const uint32_t q = e.cslen == 1 ? rem : fastdiv(rem, e.div_m, e.div_s);
+        uint32_t d = (uint32_t)e.sdig[p] + (rem - q * e.cslen) + carry;
+        carry = d >= e.cslen ? 1u : 0u;
+        d -= carry ? e.cslen : 0u;
+        rem = q;
+        dig[p * 256 + tid] = (uint8_t)d;
+    }
+    const uint32_t lim = trunc < 4u * DPRF_SLOT_WORDS ? trunc : 4u * DPRF_SLOT_WORDS;
+    uint8_t *tb = (uint8_t *)tile;
+    uint32_t pos = 0;
+    for (uint32_t p = 0; p < n; p++) {
+        const uint32_t d = dig[p * 256 + tid];
+        const uint32_t w = sym[d], k = syl[d];
+        for (uint32_t j = 0; j < k; j++, pos++)
+            if (pos < lim) tb[4u * ((pos >> 2) * 256u + tid) + (pos & 3u)] = (uint8_t)(w >> (8u * j));
+    }
+    uint4 *out = (uint4 *)(slots + (size_t)g * DPRF_SLOT_WORDS);
+#pragma unroll
+    for (int q = 0; q < DPRF_SLOT_WORDS / 4; q++)
+        out[q] = make_uint4(tile[(4 * q) * 256 + tid], tile[(4 * q + 1) * 256 + tid], tile[(4 * q + 2) * 256 + tid],
+                            tile[(4 * q + 3) * 256 + tid]);
+    lens[g] = (uint8_t)(pos < lim ? pos : lim);
+}
 #endif /* DPRF_PART_LONG */
 
 #ifdef DPRF_PART_OFFICE
@@ -1003,6 +1051,11 @@ hipError_t launch_odt(const dprf_enum &e, const dprf_odt_params &p, const dprf_a
 hipError_t launch_long_prehash(const dprf_enum &e, const dprf_long_params &lp, dprf_results *R, uint32_t cap,
                                uint32_t stop, hipStream_t s) {
     hipLaunchKernelGGL(k_long_prehash, GRID(e.count, 256), dim3(256), 0, s, e, lp, R, cap, stop);
+    return hipGetLastError();
+}
+hipError_t launch_spell_symbols(const dprf_enum &e, const uint32_t *symtab, uint32_t trunc, uint32_t *slots,
+                                uint8_t *lens, hipStream_t s) {
+    hipLaunchKernelGGL(k_spell_symbols, GRID(e.count, 256), dim3(256), 0, s, e, symtab, trunc, slots, lens);
     return hipGetLastError();
 }
 #endif

@@ -19,6 +19,11 @@ hipError_t launch_pdf_r24(const dprf_enum &e, const dprf_pdf_params &p, dprf_res
 /* long list (e.mode 2): the records' first-message hash into e.keys, or (DPRF_LONG_R5) the whole R5 check */
 hipError_t launch_long_prehash(const dprf_enum &e, const dprf_long_params &lp, dprf_results *R, uint32_t cap,
                                uint32_t stop, hipStream_t s);
+/* symbol windows (dprf_search_symbols): e.count candidates from the digits in e.sdig (base e.cslen), symbol table
+ * symtab = [256] LE-packed bytes + [256] byte counts, into slots[n][DPRF_SLOT_WORDS] / lens[n]; bytes at or past
+ * trunc stay zero */
+hipError_t launch_spell_symbols(const dprf_enum &e, const uint32_t *symtab, uint32_t trunc, uint32_t *slots,
+                                uint8_t *lens, hipStream_t s);
 hipError_t launch_pdf_r6(const dprf_enum &e, const dprf_pdf_params &p, const dprf_aes_tables *T,
                          dprf_results *R, uint32_t cap, uint32_t stop, hipStream_t s);
 #endif

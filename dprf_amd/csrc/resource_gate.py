@@ -29,6 +29,7 @@ SCRATCH_LIMIT = {
     "k_pdf_r24": 0,
     "k_pdf_r6": 0,
     "k_long_prehash": 0,      # round 4: candidates longer than a list slot
+    "k_spell_symbols": 0,     # round 6: symbol windows (dprf_search_symbols)
 }
 
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DPRF_ABI_VERSION 6
+#define DPRF_ABI_VERSION 7
 
 /* formats: the tag parse_verification_data extracts (brute_force.py:250) */
 #define DPRF_FMT_OFFICE 1   /* "$office$*2007*..."  ECMA-376 Standard Encryption            */
@@ -49,7 +49,9 @@ extern "C" {
 #define DPRF_E_PWLEN (-5)        /* candidate too long: over DPRF_MAX_PW bytes (list mode; no argv string can carry
                                     it to the reference), or a range length over DPRF_MAX_PW_RANGE  */
 #define DPRF_E_CHARSET (-6)      /* range charset invalid: empty, NUL, a repeated byte, or a byte >= 0x80
-                                    for Office (its candidates are UTF-16LE of characters)           */
+                                    for Office (its candidates are UTF-16LE of characters); symbols
+                                    (dprf_search_symbols): empty, repeated, with a NUL byte or over 4
+                                    bytes, or for Office not one valid UTF-8 character            */
 
 #define DPRF_ALL_DEVICES (-1)    /* dprf_ctx_create device argument: every gfx950 device visible    */
 #define DPRF_MAX_DEVICES 64
@@ -155,7 +157,7 @@ int dprf_ctx_last_call_devices(const dprf_ctx *ctx, dprf_device_stats *out, int 
  * character most significant).  The symbols are the charset's BYTES, all distinct (a repeated byte would
  * verify candidates twice: DPRF_E_CHARSET): for PDF and ODF a byte >= 0x80 is a raw candidate byte, as the
  * reference's argv carries it; Office takes ASCII only.  A caller whose alphabet has multi-byte UTF-8
- * characters spells the window itself and verifies it with dprf_verify_list (brute_force.search_round).
+ * characters uses dprf_search_symbols.
  * Writes up to `cap` hit indices, ascending, to hits[]; *nhits = total number of hits found (may exceed cap).
  * stats may be NULL.
  * Multi-device: the devices take contiguous chunks of the range from one shared cursor in increasing
@@ -171,6 +173,20 @@ int dprf_ctx_last_call_devices(const dprf_ctx *ctx, dprf_device_stats *out, int 
 int dprf_search_range(dprf_ctx *ctx, const uint8_t *charset, int cslen, int pwlen, uint64_t start,
                       uint64_t count, int stop_on_first, uint64_t *hits, int64_t cap, int64_t *nhits,
                       dprf_stats *stats);
+
+/* ---- range mode over multi-byte symbols (ABI 7): a --charset with non-ASCII characters ----
+ * Verifies indices [start, start+count) of sym^pwlen in itertools.product order over SYMBOLS (the last position
+ * fastest, brute_force.py:205), symbol k being the bytes sym[sym_off[k] .. sym_off[k+1]) -- a charset's characters
+ * in UTF-8, each 1-4 bytes, all distinct, no NUL byte (DPRF_E_CHARSET).  For Office each symbol must be one valid
+ * UTF-8 character and goes in as its UTF-16LE, as iconv converts the whole password (msoffcrypto...c:275-336).  The
+ * device spells every candidate into a list slot and the list-mode kernels verify it: a candidate's bytes are the
+ * concatenation of its symbols' (PDF R2-R4 hash the first 32, pdf...c:137).  DPRF_E_PWLEN: pwlen outside
+ * 1..DPRF_MAX_PW_RANGE, or a candidate could exceed a 64-byte slot after conversion and truncation (the caller
+ * spells such windows itself and uses dprf_verify_list).  hits[] are indices relative to `start`; the rest is as
+ * dprf_search_range (stop_on_first, multi-device chunks and the cross-device stop). */
+int dprf_search_symbols(dprf_ctx *ctx, const uint8_t *sym, const uint32_t *sym_off, int nsym, int pwlen,
+                        uint64_t start, uint64_t count, int stop_on_first, uint64_t *hits, int64_t cap,
+                        int64_t *nhits, dprf_stats *stats);
 
 /* ---- list mode: client payloads (init_listbased_brute_force :82-104, client.py:105) ----
  * Candidate k is blob[offsets[k] .. offsets[k+1]) (n+1 offsets).  Hits are list indices. */

@@ -248,6 +248,45 @@ def test_range_mode_finds_a_password_of_multibyte_characters(oracle, monkeypatch
     assert bf._index_to_password(0b010, "aé", 3) == "aéa"
 
 
+class _OracleSymbolCtx(_OracleBlobCtx):
+    """... plus search_symbols (ABI 7: the device spells the window by character), restated with the oracle: the
+    window spelled by payload.spell_utf8 and verified candidate by candidate.  too_long: answer E_PWLEN as the
+    library does when a candidate could exceed a 64-byte slot."""
+
+    def __init__(self, oracle, stream, log, too_long=False):
+        super().__init__(oracle, stream, log)
+        self.too_long = too_long
+
+    def search_symbols(self, charset, pwlen, start, count, stop_on_first=False, cap=1 << 16):
+        from dprf_amd import _lib
+        from dprf_amd.payload import spell_utf8
+        self.log.append(("symbols", count))
+        if self.too_long:
+            raise _lib.DprfError(_lib.E_PWLEN, "slot")
+        blob, offs = spell_utf8(charset, pwlen, start, count)
+        words = [bytes(blob[int(offs[k]):int(offs[k + 1])]) for k in range(count)]
+        h = [start + i for i, v in enumerate(self.c.verify_list(words)) if v == 1]
+        return h[:cap], len(h), {"candidates": count, "wall_ms": 1.0}
+
+
+@pytest.mark.parametrize("too_long", [False, True])
+def test_multibyte_rounds_spell_on_the_device_or_fall_back_to_the_host(oracle, monkeypatch, too_long):
+    """search_round over a multi-byte charset asks the library to spell the window (search_symbols) and returns its
+    keyspace index; when the library answers E_PWLEN (a candidate could exceed a list slot) the same round is spelled
+    on the host and verified as a list, with the same answer."""
+    stream = _planted_stream("pdf", "aéa")
+    log = []
+    ctx = _OracleSymbolCtx(oracle, stream, log, too_long=too_long)
+    monkeypatch.setattr(bf, "WIDE_ROUND", 4)
+    found, st = bf.search_round(ctx, "aé", 3, 0, 8)
+    assert found == 0b010 and bf._index_to_password(found, "aé", 3) == "aéa"
+    assert log[0] == ("symbols", 8)
+    if too_long:
+        assert [e[0] for e in log[1:]] == ["blob"] and st["candidates"] == 4     # stop_on_first: rounds of 4
+    else:
+        assert len(log) == 1 and st["candidates"] == 8
+
+
 def test_range_mode_rejects_a_bad_charset_before_device_work(monkeypatch):
     from dprf_amd import _lib
 
