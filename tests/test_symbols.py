@@ -128,3 +128,30 @@ def test_candidates_over_a_slot_are_refused_and_brute_force_spells_them_on_the_h
         assert ei.value.code == _lib.E_PWLEN
         found, _ = bf.search_round(ctx, "a\U0001D11E", 17, (1 << 17) - 4, 4)
         assert found == (1 << 17) - 1                     # the last index: every position the second symbol
+
+
+@pytest.mark.gpu
+def test_bad_symbol_tables_are_refused():
+    """DPRF_E_CHARSET before any device work: empty, repeated, NUL-carrying or over-4-byte symbols; for Office a symbol
+    that is not one valid UTF-8 character (its UTF-16LE would be undefined, msoffcrypto...c:287-336)."""
+    import ctypes
+    from dprf_amd import _lib
+    L = _lib.lib()
+
+    def call(ctx, syms, pwlen=2):
+        offs = [0]
+        for b in syms:
+            offs.append(offs[-1] + len(b))
+        nh = ctypes.c_int64()
+        hits = (ctypes.c_uint64 * 1)()
+        return L.dprf_search_symbols(ctx._h, b"".join(syms), (ctypes.c_uint32 * len(offs))(*offs), len(syms), pwlen,
+                                     0, 4, 0, hits, 1, ctypes.byref(nh), None)
+    with _lib.Context(_fields(_doc("pdf", {"R": 4, "length": 128}, PW)), device=0) as ctx:
+        for bad in ([b"a", b""], [b"a", b"a"], [b"a\x00"], [b"abcde"], []):
+            assert call(ctx, bad) == _lib.E_CHARSET, bad
+        assert call(ctx, [b"\xc3", b"\xa9"]) == 0           # PDF: raw byte symbols are symbols
+        assert call(ctx, [b"a", b"b"], pwlen=33) == _lib.E_PWLEN
+    with _lib.Context(_fields(_doc("docx", {}, PW)), device=0) as ctx:
+        for bad in ([b"\xc3"], [b"ab"], [b"\xed\xa0\x80"]):  # truncated, two characters, a lone surrogate
+            assert call(ctx, bad) == _lib.E_CHARSET, bad
+        assert call(ctx, ["é".encode(), "\U0001D11E".encode()]) == 0
