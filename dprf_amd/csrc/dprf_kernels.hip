@@ -757,6 +757,30 @@ k_pdf_r5(dprf_enum e, dprf_pdf_params p, dprf_results *R, uint32_t cap, uint32_t
             if (sha256_block_matches(b, p.u, valid)) report_hit(e, R, e.start + g, cap, stop_on_first);
             continue;
         }
+        if (NW < 8) {
+            /* a list launch whose candidates all have at most 4 NW <= 16 bytes (launch_pdf_r5 picks NW from the
+             * launch's longest): one message block, words past NW + 2 zero, and the round-61 early exit */
+            uint32_t b[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) b[j] = j < NW ? (c.w[j] & le_keep_mask(j, c.len)) : 0u;
+            const uint32_t sw[3] = {p.u[8], p.u[9], 0x80u};
+            const uint32_t q = c.len >> 2, r = (c.len & 3u) * 8u;
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                const uint32_t lo = r ? (sw[s] << r) : sw[s];
+                const uint32_t hi = r ? (sw[s] >> (32u - r)) : 0u;
+#pragma unroll
+                for (int j = 0; j < NW + 3; j++) {
+                    if ((uint32_t)j == q + s) b[j] |= lo;
+                    if ((uint32_t)j == q + s + 1) b[j] |= hi;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NW + 3; j++) b[j] = bswap32(b[j]);
+            b[15] = (c.len + 8u) * 8u;
+            if (sha256_block_matches(b, p.u, valid)) report_hit(e, R, e.start + g, cap, stop_on_first);
+            continue;
+        }
         /* SHA256(pw[:127] || U[32:40]) == U[0:32] (pdf...c:194-221); host caps len at 127 and slots at 64 */
         uint32_t m[32];
 #pragma unroll
@@ -1073,6 +1097,10 @@ hipError_t launch_pdf_r5(const dprf_enum &e, const dprf_pdf_params &p, dprf_resu
         case 4: L5W(4); break;
         default: L5W(8); break;
         }
+    } else if (e.mode == 1 && e.pwlen <= 8) {
+        L5(1, 2, 8);
+    } else if (e.mode == 1 && e.pwlen <= 16) {
+        L5(1, 4, 8);
     } else {
         L5(1, 8, 8);
     }
