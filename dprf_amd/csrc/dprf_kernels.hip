@@ -225,47 +225,63 @@ k_long_prehash(dprf_enum e, dprf_long_params lp, dprf_results *R, uint32_t cap, 
  * character, its UTF-8 -- for Office its UTF-16LE -- bytes): index g of the chunk -> the candidate's bytes in a list
  * slot, in itertools.product order over the symbols (brute_force.py:205), for the list-mode kernels to verify.  The
  * digits come as in range_candidate (the chunk start's digits from the host, g added with carries); the bytes are
- * assembled in the thread's column of an LDS tile ([word][thread]: conflict-free) and stored as four 16-byte words.
+ * assembled in the thread's column of an LDS tile and the block's slots leave it as consecutive 16-byte pieces.
  * Bytes at or past `trunc` (PDF R2-R4 hash 32, pdf...c:137) and past the slot are never written: the slot stays zero
  * there, as dprf_verify_list packs a truncated candidate. */
 __global__ void __launch_bounds__(256)
 k_spell_symbols(dprf_enum e, const uint32_t *symtab, uint32_t trunc, uint32_t *slots, uint8_t *lens) {
+    /* the block's 256 slots as [word][slot] with a row stride of 258 words: the byte stores of one word index and the
+     * 16-byte read-outs below both spread over the banks */
+    constexpr uint32_t ST = 258;
     __shared__ uint32_t sym[256], syl[256];
-    __shared__ uint32_t tile[DPRF_SLOT_WORDS * 256];
-    __shared__ uint8_t dig[DPRF_MAX_RANGE_LEN * 256];
+    __shared__ uint32_t tile[DPRF_SLOT_WORDS * ST];
     const uint32_t tid = threadIdx.x;
     sym[tid] = symtab[tid];
     syl[tid] = symtab[256 + tid];
 #pragma unroll
-    for (int j = 0; j < DPRF_SLOT_WORDS; j++) tile[j * 256 + tid] = 0u;
+    for (int j = 0; j < DPRF_SLOT_WORDS; j++) tile[j * ST + tid] = 0u;
     __syncthreads();
     const uint32_t g = blockIdx.x * 256u + tid;
-    if (g >= e.count) return;
     const uint32_t n = e.pwlen < DPRF_MAX_RANGE_LEN ? e.pwlen : DPRF_MAX_RANGE_LEN;
-    uint32_t rem = g, carry = 0;
-    for (int p = (int)n - 1; p >= 0; --p) {
-        const uint32_t q = e.cslen == 1 ? rem : fastdiv(rem, e.div_m, e.div_s);
-        uint32_t d = (uint32_t)e.sdig[p] + (rem - q * e.cslen) + carry;
-        carry = d >= e.cslen ? 1u : 0u;
-        d -= carry ? e.cslen : 0u;
-        rem = q;
-        dig[p * 256 + tid] = (uint8_t)d;
-    }
     const uint32_t lim = trunc < 4u * DPRF_SLOT_WORDS ? trunc : 4u * DPRF_SLOT_WORDS;
-    uint8_t *tb = (uint8_t *)tile;
-    uint32_t pos = 0;
-    for (uint32_t p = 0; p < n; p++) {
-        const uint32_t d = dig[p * 256 + tid];
-        const uint32_t w = sym[d], k = syl[d];
-        for (uint32_t j = 0; j < k; j++, pos++)
-            if (pos < lim) tb[4u * ((pos >> 2) * 256u + tid) + (pos & 3u)] = (uint8_t)(w >> (8u * j));
+    if (g < e.count) {
+        /* the digits twice, last position first (as range_candidate): once for the length, once to store each
+         * symbol's bytes right to left from it -- no digit array */
+        uint32_t total = 0;
+        for (int pass = 0; pass < 2; pass++) {
+            uint32_t rem = g, carry = 0, pos = total;
+            for (int p = (int)n - 1; p >= 0; --p) {
+                const uint32_t q = e.cslen == 1 ? rem : fastdiv(rem, e.div_m, e.div_s);
+                uint32_t d = (uint32_t)e.sdig[p] + (rem - q * e.cslen) + carry;
+                carry = d >= e.cslen ? 1u : 0u;
+                d -= carry ? e.cslen : 0u;
+                rem = q;
+                const uint32_t k = syl[d];
+                if (pass == 0) {
+                    total += k;
+                } else {
+                    pos -= k;
+                    const uint32_t w = sym[d];
+                    uint8_t *tb = (uint8_t *)tile;
+                    for (uint32_t j = 0; j < k; j++)
+                        if (pos + j < lim) tb[4u * (((pos + j) >> 2) * ST + tid) + ((pos + j) & 3u)] = (uint8_t)(w >> (8u * j));
+                }
+            }
+        }
+        lens[g] = (uint8_t)(total < lim ? total : lim);
     }
-    uint4 *out = (uint4 *)(slots + (size_t)g * DPRF_SLOT_WORDS);
+    __syncthreads();
+    /* read-out: 16-byte piece u = 256 q + tid of the block's 16 KB of slots (slot u / 4, words 4 (u % 4) ..), so every
+     * store instruction of the block writes 4 KB of consecutive memory */
+    const uint32_t base = blockIdx.x * 256u;
+    uint4 *out = (uint4 *)(slots + (size_t)base * DPRF_SLOT_WORDS);
 #pragma unroll
-    for (int q = 0; q < DPRF_SLOT_WORDS / 4; q++)
-        out[q] = make_uint4(tile[(4 * q) * 256 + tid], tile[(4 * q + 1) * 256 + tid], tile[(4 * q + 2) * 256 + tid],
-                            tile[(4 * q + 3) * 256 + tid]);
-    lens[g] = (uint8_t)(pos < lim ? pos : lim);
+    for (int q = 0; q < 4; q++) {
+        const uint32_t u = 256u * q + tid, sl = u >> 2, w0 = 4u * (u & 3u);
+        if (base + sl < e.count)
+            out[u] = make_uint4(tile[w0 * ST + sl], tile[(w0 + 1) * ST + sl], tile[(w0 + 2) * ST + sl],
+                                tile[(w0 + 3) * ST + sl]);
+    }
 }
 #endif /* DPRF_PART_LONG */
 
