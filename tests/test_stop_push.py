@@ -116,3 +116,26 @@ def test_one_lane_reports_the_hit_time():
         assert hits[:1] == [IDX] and 0 <= st["hit_ms"] <= st["wall_ms"], st
         hits, _, st = ctx.search_range(LOWER, 5, 1 << 20, 1 << 16, stop_on_first=True, cap=4)
         assert hits == [] and st["hit_ms"] == -1, st
+
+
+@pytest.mark.gpu
+def test_a_hit_stops_the_other_lanes_in_a_symbol_window():
+    """The same for a device-spelled symbol window (ABI 7): ODF, 2-byte characters, the password early in lane 0's
+    first chunk of a 2^22-candidate window on two lanes."""
+    import docgen
+    from dprf_amd import _lib
+    from dprf_amd.parsers import odt2hashes
+    cs = "αβγδεζηθικλμνξοπρστυφχψω"
+    pw = "ααβγ" + "δε"
+    with tempfile.TemporaryDirectory() as t:
+        docgen.write_odt(os.path.join(t, "d.odt"), pw, 0x5709)
+        stream = odt2hashes.get_hashes(os.path.join(t, "d.odt"), False)
+    idx = sum(cs.index(ch) * len(cs) ** (5 - k) for k, ch in enumerate(pw))
+    with _lib.Context(_fields(stream), devices=[0, 0]) as ctx:
+        hits, _, st = ctx.search_symbols(cs, 6, 0, 1 << 22, stop_on_first=True, cap=4)
+        per = ctx.last_call_devices()
+    assert hits[:1] == [idx] and st["stopped_early"] == 1, (hits, st)
+    assert per[1]["evaluated"] <= GEN, per
+    _record("odt_symbols_lanes2", {"hit_ms": st["hit_ms"], "wall_ms": st["wall_ms"],
+                                   "after_hit_ms": st["wall_ms"] - st["hit_ms"],
+                                   "evaluated": [d["evaluated"] for d in per], "launched": [d["candidates"] for d in per]})
