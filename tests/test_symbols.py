@@ -155,3 +155,25 @@ def test_bad_symbol_tables_are_refused():
         for bad in ([b"\xc3"], [b"ab"], [b"\xed\xa0\x80"]):  # truncated, two characters, a lone surrogate
             assert call(ctx, bad) == _lib.E_CHARSET, bad
         assert call(ctx, ["é".encode(), "\U0001D11E".encode()]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,kw", [("odt", {}), ("docx", {}), ("pdf", {"R": 6, "length": 256}),
+                                     ("pdf", {"R": 5, "length": 256})], ids=["odt", "office", "pdf-r6", "pdf-r5"])
+def test_slot_filling_symbol_candidates(kind, kw):
+    """Candidates of up to exactly 64 bytes (16 four-byte characters: the SHA terminator falls in the word after the
+    slot, the round-5 slot-edge bug class) and 60 bytes, spelled on the device: the planted password found at its
+    index, the same hits as the host-spelled list."""
+    from dprf_amd import _lib
+    from dprf_amd.payload import spell_utf8
+    cs = "a\U0001D11E"
+    for n in (16, 15):
+        pw = "\U0001D11E" * n                                  # 4n bytes of UTF-8 (Office: 4n of UTF-16LE)
+        stream = _doc(kind, kw, pw)
+        idx = (1 << n) - 1
+        s, cnt = (1 << n) - 64, 64
+        blob, offs = spell_utf8(cs, n, s, cnt)
+        with _lib.Context(_fields(stream), device=0) as ctx:
+            hs, _, _ = ctx.search_symbols(cs, n, s, cnt)
+            hl, _, _ = ctx.verify_blob(blob, offs)
+        assert hs == [idx] == [s + h for h in hl], (kind, n, hs, hl)
